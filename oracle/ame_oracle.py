@@ -1,0 +1,285 @@
+"""CPU oracle for the temporal-AME structured/naive mean-field VI hot path.
+
+TEST INFRASTRUCTURE ONLY.  This module is a plain-numpy restatement of the
+reference algorithm (Alfieriek/Python-Temporal-AME-SVI, ``src/inference``).
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
+leg may import it, and only as the checker / CPU baseline.  The product path
+(``ame_amd``) never imports it and fails loudly without its HIP library.
+
+Parity pin: every function below is checked against golden fixtures produced by
+running the reference itself (``tests/golden/make_golden.py`` imports
+/root/reference in the build container and writes ``tests/golden/*.npz``).
+See ``tests/test_oracle_golden.py``.
+
+Layout follows the reference: ``X_mean (n, T, d)``, ``X_cov (n, T, d, d)``,
+``Y (n, n, T, 2)``, state ``x = [a, b, U(r), V(r)]``, ``d = 2 + 2r``
+(src/models/temporal_ame.py:114-120).
+
+The arithmetic dtype is the dtype of the arrays passed in (float32 mirrors the
+reference's default dtype; float64 is the "fp64 oracle" of SURVEY App. C).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+LOG2PI = math.log(2.0 * math.pi)
+
+
+# ----------------------------------------------------------------------------
+# model constants (src/models/base.py:123-196, static_ame.py:96-127,
+# temporal_ame.py:129-145)
+# ----------------------------------------------------------------------------
+def cov_matrix(dim, correlation, variance, dtype=np.float32):
+    """BaseAMEModel._generate_covariance_matrix (src/models/base.py:123-153)."""
+    c = np.full((dim, dim), correlation * variance, dtype=dtype)
+    np.fill_diagonal(c, variance)
+    return c
+
+
+def model_params(r, ar=0.8, rho_add=0.5, rho_mult=0.3, rho_dyadic=0.5,
+                 process_noise_scale=0.1, dtype=np.float32):
+    """R, R_inv, Sigma, Psi, Phi, Q exactly as the reference model builds them."""
+    d = 2 + 2 * r
+    # R overrides the base-class R (static_ame.py:96-101): var 0.1, corr rho_dyadic.
+    R = cov_matrix(2, rho_dyadic, 0.1, dtype)
+    R_inv = np.linalg.inv(R.astype(np.float64)).astype(dtype)
+    Sigma = cov_matrix(2, rho_add, 1.0, dtype)                     # static_ame.py:111-118
+    Psi = np.zeros((2 * r, 2 * r), dtype)                           # static_ame.py:120-127
+    Psi[:r, :r] = cov_matrix(r, rho_mult, 1.0, dtype)
+    Psi[r:, r:] = cov_matrix(r, rho_mult, 1.0, dtype)
+    Phi = np.eye(d, dtype=dtype) * dtype(ar)                          # temporal_ame.py:132
+    S0 = sigma0(Sigma, Psi)
+    Q = (S0 * dtype(1 - ar ** 2)) * dtype(process_noise_scale)     # temporal_ame.py:144-145
+    return dict(R=R, R_inv=R_inv, Sigma=Sigma, Psi=Psi, Phi=Phi, Q=Q)
+
+
+def sigma0(Sigma, Psi):
+    """blockdiag(Sigma, Psi) as built in structured_mf.py:234-236."""
+    d = 2 + Psi.shape[0]
+    S0 = np.zeros((d, d), dtype=Sigma.dtype)
+    S0[:2, :2] = Sigma
+    S0[2:, 2:] = Psi
+    return S0
+
+
+def _inv(a):
+    return np.linalg.inv(a)
+
+
+def _logdet(a):
+    """torch.logdet semantics: nan for negative determinant, -inf for zero."""
+    sign, ld = np.linalg.slogdet(a.astype(np.float64))
+    if sign < 0:
+        return float("nan")
+    if sign == 0:
+        return float("-inf")
+    return float(ld)
+
+
+# ----------------------------------------------------------------------------
+# observation terms (structured_mf.py:289-326 / naive_mf.py:284-376)
+# ----------------------------------------------------------------------------
+def observation_terms(Y, X_mean, R_inv, i, t):
+    """P_obs = sum_{j!=i} J^T R^-1 J, h_obs = sum_{j!=i} J^T R^-1 y_ij.
+
+    J_j = [[1, 0, V_j, 0], [0, 1, 0, U_j]] (structured_mf.py:309-320).  Summed over
+    all j != i with the *current* means (new for j < i inside a sweep).
+    """
+    n, T, d = X_mean.shape
+    r = (d - 2) // 2
+    dt = X_mean.dtype
+    mask = np.ones(n, dtype=bool)
+    mask[i] = False
+    M = X_mean[mask, t, 2:]
+    U, V = M[:, :r], M[:, r:]
+    m = M.shape[0]
+    E0 = np.zeros((m, d), dt)
+    E1 = np.zeros((m, d), dt)
+    E0[:, 0] = 1
+    E0[:, 2:2 + r] = V
+    E1[:, 1] = 1
+    E1[:, 2 + r:] = U
+    p, q, s = R_inv[0, 0], R_inv[0, 1], R_inv[1, 1]
+    q2 = R_inv[1, 0]
+    P = p * (E0.T @ E0) + q * (E0.T @ E1) + q2 * (E1.T @ E0) + s * (E1.T @ E1)
+    y = Y[i, mask, t, :]                     # (m, 2)
+    z = y @ R_inv.T                          # z_j = R_inv @ y_ij
+    h = E0.T @ z[:, 0] + E1.T @ z[:, 1]
+    return P.astype(dt), h.astype(dt)
+
+
+def prior_terms(params, T, dtype):
+    Q_inv = _inv(params["Q"]).astype(dtype)
+    S0_inv = _inv(sigma0(params["Sigma"], params["Psi"])).astype(dtype)
+    Phi = params["Phi"]
+    PtQiP = (Phi.T @ (Q_inv @ Phi)).astype(dtype)
+    return Q_inv, S0_inv, PtQiP
+
+
+# ----------------------------------------------------------------------------
+# the sweep (structured_mf.py:211-287, naive_mf.py:193-282)
+# ----------------------------------------------------------------------------
+def update_node(Y, X_mean, X_cov, params, i, variant, lr, consts=None):
+    """One node's forward sweep over t, in place.  variant in {good, bad, naive}."""
+    n, T, d = X_mean.shape
+    dt = X_mean.dtype
+    Q_inv, S0_inv, PtQiP = consts if consts is not None else prior_terms(params, T, dt)
+    Phi = params["Phi"]
+    R_inv = params["R_inv"]
+    eye = np.eye(d, dtype=dt)
+    for t in range(T):
+        P_obs, h_obs = observation_terms(Y, X_mean, R_inv, i, t)
+        P = P_obs.copy()
+        h = h_obs.copy()
+        if t == 0:
+            P = P + S0_inv
+        if t > 0:
+            P = P + Q_inv
+            h = h + Q_inv @ (Phi @ X_mean[i, t - 1])
+        if t < T - 1:
+            P = P + PtQiP
+            h = h + Phi.T @ (Q_inv @ X_mean[i, t + 1])
+        if variant == "naive":
+            mu = np.linalg.solve(P, h)
+            C = np.diag(dt.type(1.0) / (np.diag(P) + dt.type(1e-8))).astype(dt)
+        else:
+            C = _inv(P)
+            if variant == "bad":
+                C[:2, 2:] = 0
+                C[2:, :2] = 0
+            C = (C + C.T) / dt.type(2)
+            C = C + eye * dt.type(1e-6)
+            mu = C @ h
+        X_mean[i, t] = dt.type(lr) * mu + dt.type(1 - lr) * X_mean[i, t]
+        X_cov[i, t] = dt.type(lr) * C + dt.type(1 - lr) * X_cov[i, t]
+
+
+def sweep(Y, X_mean, X_cov, params, variant, lr, nodes=None):
+    """_update_step: sequential Gauss-Seidel over nodes (structured_mf.py:217-218)."""
+    n, T, d = X_mean.shape
+    consts = prior_terms(params, T, X_mean.dtype)
+    for i in (range(n) if nodes is None else nodes):
+        update_node(Y, X_mean, X_cov, params, i, variant, lr, consts)
+
+
+# ----------------------------------------------------------------------------
+# ELBO (structured_mf.py:115-209; naive_mf.py:89-191) and recon
+# (temporal_ame.py:255-291)
+# ----------------------------------------------------------------------------
+def compute_mean(X_t, r):
+    """StaticAMEModel.compute_mean (static_ame.py:189-238) for one time slice."""
+    a, b = X_t[:, 0], X_t[:, 1]
+    U, V = X_t[:, 2:2 + r], X_t[:, 2 + r:]
+    add = a[:, None] + b[None, :]
+    mult = U @ V.T
+    mu = np.empty(add.shape + (2,), dtype=X_t.dtype)
+    mu[:, :, 0] = add + mult
+    mu[:, :, 1] = add.T + mult.T
+    return mu
+
+
+def expected_loglik(Y, X_mean, X_cov, params, variant, ts=None):
+    n, T, d = X_mean.shape
+    r = (d - 2) // 2
+    R_inv = params["R_inv"].astype(np.float64)
+    logdetR = _logdet(params["R"])
+    trRi = float(np.trace(R_inv))
+    iu, ju = np.triu_indices(n, k=1)
+    total = 0.0
+    for t in (range(T) if ts is None else ts):
+        mu = compute_mean(X_mean[:, t].astype(np.float64), r)
+        res = Y[iu, ju, t, :].astype(np.float64) - mu[iu, ju]
+        quad = np.einsum("pa,ab,pb->p", res, R_inv, res)
+        if variant == "naive":
+            corr = 0.0
+        else:
+            tr = np.trace(X_cov[:, t].astype(np.float64), axis1=1, axis2=2)
+            corr = 0.1 * (tr[iu] + tr[ju]) * trRi / d
+        total += float(np.sum(-0.5 * (logdetR + quad + corr + 2 * LOG2PI)))
+    return total
+
+
+def log_prior_initial(X_mean, X_cov, params):
+    n, T, d = X_mean.shape
+    S0 = sigma0(params["Sigma"], params["Psi"]).astype(np.float64)
+    S0i = np.linalg.inv(S0)
+    ld = _logdet(S0)
+    mu0 = X_mean[:, 0].astype(np.float64)
+    quad = np.einsum("na,ab,nb->n", mu0, S0i, mu0)
+    tr = np.einsum("ab,nba->n", S0i, X_cov[:, 0].astype(np.float64))
+    return float(np.sum(-0.5 * (ld + quad + tr + d * LOG2PI)))
+
+
+def log_prior_transitions(X_mean, X_cov, params):
+    n, T, d = X_mean.shape
+    if T < 2:
+        return 0.0
+    Q = params["Q"].astype(np.float64)
+    Qi = np.linalg.inv(Q)
+    ld = _logdet(Q)
+    Phi = params["Phi"].astype(np.float64)
+    Xm = X_mean.astype(np.float64)
+    res = Xm[:, 1:] - np.einsum("ab,ntb->nta", Phi, Xm[:, :-1])
+    quad = np.einsum("nta,ab,ntb->nt", res, Qi, res)
+    tr = np.einsum("ab,ntba->nt", Qi, X_cov[:, 1:].astype(np.float64))
+    return float(np.sum(-0.5 * (ld + quad + tr + d * LOG2PI)))
+
+
+def entropy(X_cov):
+    n, T, d, _ = X_cov.shape
+    tot = 0.0
+    for i in range(n):
+        for t in range(T):
+            tot += 0.5 * (d * (1 + LOG2PI) + _logdet(X_cov[i, t]))
+    return tot
+
+
+def elbo_split(Y, X_mean, X_cov, params, variant):
+    return np.array([
+        expected_loglik(Y, X_mean, X_cov, params, variant),
+        log_prior_initial(X_mean, X_cov, params),
+        log_prior_transitions(X_mean, X_cov, params),
+        entropy(X_cov),
+    ])
+
+
+def elbo(Y, X_mean, X_cov, params, variant):
+    return float(np.sum(elbo_split(Y, X_mean, X_cov, params, variant)))
+
+
+def recon_error(Y, X_mean):
+    """compute_temporal_reconstruction_error (temporal_ame.py:255-291)."""
+    n, T, d = X_mean.shape
+    r = (d - 2) // 2
+    off = ~np.eye(n, dtype=bool)
+    tot = 0.0
+    for t in range(T):
+        mu = compute_mean(X_mean[:, t].astype(np.float64), r)
+        e = (Y[:, :, t].astype(np.float64) - mu) ** 2
+        tot += float(e[off].sum())
+    return tot / (n * (n - 1) * T)
+
+
+# ----------------------------------------------------------------------------
+# fit (base.py:127-208) without printing
+# ----------------------------------------------------------------------------
+def fit(Y, X_mean, X_cov, params, variant, lr, max_iter, tolerance=1e-4):
+    hist = {"elbo": [], "reconstruction_error": []}
+    prev = -np.inf
+    patience = 0
+    for it in range(max_iter):
+        sweep(Y, X_mean, X_cov, params, variant, lr)
+        e = elbo(Y, X_mean, X_cov, params, variant)
+        hist["elbo"].append(e)
+        hist["reconstruction_error"].append(recon_error(Y, X_mean))
+        converged = False
+        if it > 0:
+            rel = abs(e - prev) / (abs(prev) + 1e-8)
+            patience = patience + 1 if rel < tolerance else 0
+            converged = patience >= 3
+        prev = e
+        if converged:
+            break
+    return hist
