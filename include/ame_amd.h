@@ -1,0 +1,161 @@
+/*
+ * ame_amd.h — C ABI of the MI355X (gfx950) implementation of the temporal-AME
+ * structured / naive mean-field VI hot path.
+ *
+ * Drop-in boundary.  The reference (Alfieriek/Python-Temporal-AME-SVI) is pure
+ * Python: its "interface" for this path is the template-method hooks of
+ * BaseVariationalInference (src/inference/base.py:84-125) that fit()
+ * (base.py:127-208) calls once per iteration.  Each entry point below replaces
+ * one of those hooks (or the loop nest inside it); the Python host classes in
+ * ame_amd/inference mirror the reference classes on top of this ABI.
+ *
+ *   ame_pack_y        replaces nothing in the reference: relayout of the
+ *                     observed network Y (n,n,T,2) (temporal_ame.py:174) into
+ *                     the time-major (T,n,n,2) layout the kernels stream.
+ *   ame_sweep         replaces _update_step -> _update_node_i ->
+ *                     _compute_observation_terms (structured_mf.py:211-326,
+ *                     naive_mf.py:193-376): the sequential Gauss-Seidel sweep,
+ *                     means only.
+ *   ame_cov           replaces the covariance half of _update_node_i
+ *                     (structured_mf.py:266-287; naive_mf.py:270-282) and
+ *                     produces the per-(node,time) covariance terms of the ELBO
+ *                     (_compute_entropy :202-209, trace terms :142-144, :166,
+ *                     :193).
+ *   ame_elbo          replaces _compute_elbo (structured_mf.py:115-209,
+ *                     naive_mf.py:89-191) and
+ *                     compute_temporal_reconstruction_error
+ *                     (temporal_ame.py:255-291): returns the sufficient sums
+ *                     from which the host assembles ELBO and MSE.
+ *
+ * Conventions: all pointers are DEVICE pointers (hipMalloc / torch CUDA
+ * tensors) unless the field says otherwise; `stream` is a hipStream_t (NULL =
+ * default stream); no entry point allocates, frees or synchronises.  Return
+ * value 0 = launched; negative = argument error (see ame_last_error()).
+ * Device-side failures (spin timeout, non-finite pivot) are reported through
+ * the `status` word, which the host reads after the iteration.
+ *
+ * Layouts (row-major, fp32 unless stated):
+ *   Yt      [T_local][n][n][2]    Yt[t][i][j] = Y[i][j][t0+t] of the reference
+ *   X mean  [T_local][n][d]       d = 2 + 2r, x = [a, b, U(r), V(r)]
+ *   X cov   [T_local][n][d][d]
+ *   consts  fp64 [5][d][d]: S0inv, Qinv, PhiT*Qinv*Phi, Qinv*Phi, PhiT*Qinv
+ */
+#ifndef AME_AMD_H
+#define AME_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum ame_variant { AME_GOOD = 0, AME_BAD = 1, AME_NAIVE = 2 };
+
+/* status word bits (device-written) */
+#define AME_STATUS_SPIN_TIMEOUT 1u
+#define AME_STATUS_HALO_TIMEOUT 2u
+
+typedef struct ame_dims {
+    int32_t n;        /* nodes */
+    int32_t r;        /* latent_dim; d = 2 + 2r */
+    int32_t T_local;  /* time slices held by this rank */
+    int32_t t_begin;  /* global index of local slice 0 */
+    int32_t T_total;  /* global number of time steps */
+    int32_t variant;  /* enum ame_variant */
+} ame_dims;
+
+typedef struct ame_sweep_args {
+    const float* Yt;             /* [T_local][n][n][2] */
+    const float* x_old;          /* [T_local][n][d] means before the sweep */
+    float* x_new;                /* [T_local][n][d] means after the sweep */
+    const float* next_old;       /* [n][d] old means at global slice t_begin+T_local
+                                    (right halo), NULL if this rank holds T-1 */
+    uint64_t* hand;              /* [T_local][n][d] {epoch,value} granules, lane hand-off */
+    const uint64_t* halo_in;     /* [n][d] granules of slice t_begin-1 (left rank), or NULL */
+    uint64_t* halo_out;          /* [n][d] granules of slice t_begin+T_local-1 for the right
+                                    rank (peer/host-mapped), or NULL */
+    double* snap;                /* [T_local][ceil(n/16)][2r+3r^2] fp64 statistic snapshots */
+    const double* consts;        /* fp64 [5][d][d] */
+    double rinv[4];              /* R_inv row-major (host values) */
+    float lr;                    /* learning_rate (damping) */
+    float one_minus_lr;          /* (float)(1 - lr) computed in double on the host */
+    uint32_t epoch;              /* sweep counter, >= 1, identical on every rank */
+    uint32_t* status;            /* [1] error word */
+} ame_sweep_args;
+
+typedef struct ame_cov_args {
+    const float* x_old;          /* [T_local][n][d] */
+    const float* x_new;          /* [T_local][n][d] */
+    float* cov;                  /* [T_local][n][d][d] updated in place */
+    const double* snap;          /* as written by ame_sweep */
+    const double* consts;        /* fp64 [5][d][d] */
+    double* cov_terms;           /* [T_local][n][4] fp64: logdet, trace, tr(Qinv S), tr(S0inv S) */
+    double rinv[4];
+    float lr;
+    float one_minus_lr;
+    int32_t update;              /* 1: damped update from the sweep; 0: terms of cov as-is */
+} ame_cov_args;
+
+typedef struct ame_elbo_args {
+    const float* Yt;             /* [T_local][n][n][2] */
+    const float* x;              /* [T_local][n][d] means */
+    const float* prev_final;     /* [n][d] means at global slice t_begin-1 (left halo) or NULL */
+    const double* cov_terms;     /* [T_local][n][4] from ame_cov */
+    const double* consts;        /* fp64 [5][d][d] */
+    const double* phi;           /* fp64 [d][d] Phi */
+    double rinv[4];
+    int32_t swap_consistent;     /* 1: Y[j][i] == swap(Y[i][j]) for all pairs (checked at pack) */
+    double* work;                /* scratch, >= ame_elbo_work_size() doubles */
+    double* out;                 /* [8] sufficient sums (see ame_elbo doc) */
+} ame_elbo_args;
+
+/* Relayout Y [n][n][T_total][2] -> Yt [T_local][n][n][2] for slices
+ * [t_begin, t_begin+T_local), and count pairs with Y[j][i] != swap(Y[i][j])
+ * into *mismatch (device uint64, caller zeroes it). */
+int ame_pack_y(const float* Y, float* Yt, const ame_dims* dims,
+               unsigned long long* mismatch, void* stream);
+
+/* One Gauss-Seidel sweep over all n nodes for the local slices (means only).
+ * One workgroup per local slice; all T_local workgroups must be co-resident
+ * (see ame_sweep_max_slices).  Reproduces the reference node order exactly:
+ * step (i,t) sees new means of nodes j<i at t and of node i at t-1, and old
+ * means of nodes j>i at t and of node i at t+1. */
+int ame_sweep(const ame_dims* dims, const ame_sweep_args* args, void* stream);
+
+/* Largest T_local ame_sweep can run with for (n, r) on this device, 0 if the
+ * per-slice state does not fit one workgroup. */
+int ame_sweep_max_slices(int n, int r);
+
+/* Dynamic LDS bytes ame_sweep needs per workgroup (0 = unsupported r). */
+long long ame_sweep_lds_bytes(int n, int r);
+
+/* Covariance update for every (node, local slice) in parallel, reconstructing
+ * each step's precision from the sweep's statistic snapshots (bit-identical to
+ * the precision the sweep solved with), plus the per-(node,time) covariance
+ * terms of the ELBO. */
+int ame_cov(const ame_dims* dims, const ame_cov_args* args, void* stream);
+
+/* ELBO / reconstruction sufficient sums over the local slices:
+ *  out[0] sum_{t, i<j} r^T Rinv r          out[1] sum_{i,t} tr(S_it)
+ *  out[2] sum_i mu_i0^T S0inv mu_i0        out[3] sum_i tr(S0inv S_i0)
+ *  out[4] sum_{i,t>=1} e^T Qinv e          out[5] sum_{i,t>=1} tr(Qinv S_it)
+ *  out[6] sum_{i,t} logdet S_it            out[7] sum_{t, i!=j} |Y_ij - m_ij|^2
+ * (slice-0 / t>=1 terms use global time; the host adds the constants). */
+int ame_elbo(const ame_dims* dims, const ame_elbo_args* args, void* stream);
+
+/* Scratch doubles ame_elbo needs. */
+long long ame_elbo_work_size(const ame_dims* dims);
+
+/* Latent dims compiled into this library (fills up to cap entries, returns count). */
+int ame_supported_r(int* out, int cap);
+
+/* Human-readable message for the last argument error on this thread. */
+const char* ame_last_error(void);
+
+/* Build/version string (includes the offload arch). */
+const char* ame_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AME_AMD_H */

@@ -1,0 +1,101 @@
+"""ctypes binding of libame_amd.so (C ABI declared in include/ame_amd.h).
+
+The product path has no CPU fallback: if the HIP library is missing or cannot
+be loaded, :func:`lib` raises ``RuntimeError`` with the reason.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libame_amd.so")
+
+AME_GOOD, AME_BAD, AME_NAIVE = 0, 1, 2
+AME_STATUS_SPIN_TIMEOUT = 1
+AME_STATUS_HALO_TIMEOUT = 2
+
+c_int32 = ctypes.c_int32
+c_vp = ctypes.c_void_p
+
+
+class ame_dims(ctypes.Structure):
+    _fields_ = [("n", c_int32), ("r", c_int32), ("T_local", c_int32), ("t_begin", c_int32),
+                ("T_total", c_int32), ("variant", c_int32)]
+
+
+class ame_sweep_args(ctypes.Structure):
+    _fields_ = [("Yt", c_vp), ("x_old", c_vp), ("x_new", c_vp), ("next_old", c_vp),
+                ("hand", c_vp), ("halo_in", c_vp), ("halo_out", c_vp), ("snap", c_vp),
+                ("consts", c_vp), ("rinv", ctypes.c_double * 4), ("lr", ctypes.c_float),
+                ("one_minus_lr", ctypes.c_float), ("epoch", ctypes.c_uint32), ("status", c_vp)]
+
+
+class ame_cov_args(ctypes.Structure):
+    _fields_ = [("x_old", c_vp), ("x_new", c_vp), ("cov", c_vp), ("snap", c_vp),
+                ("consts", c_vp), ("cov_terms", c_vp), ("rinv", ctypes.c_double * 4),
+                ("lr", ctypes.c_float), ("one_minus_lr", ctypes.c_float), ("update", c_int32)]
+
+
+class ame_elbo_args(ctypes.Structure):
+    _fields_ = [("Yt", c_vp), ("x", c_vp), ("prev_final", c_vp), ("cov_terms", c_vp),
+                ("consts", c_vp), ("phi", c_vp), ("rinv", ctypes.c_double * 4),
+                ("swap_consistent", c_int32), ("work", c_vp), ("out", c_vp)]
+
+
+# every symbol include/ame_amd.h declares (checked by tests/test_capi.py)
+EXPORTS = ("ame_pack_y", "ame_sweep", "ame_sweep_max_slices", "ame_sweep_lds_bytes", "ame_cov",
+           "ame_elbo", "ame_elbo_work_size", "ame_supported_r", "ame_last_error", "ame_version")
+
+_lock = threading.Lock()
+_lib = None
+
+
+def _declare(L):
+    P = ctypes.POINTER
+    L.ame_pack_y.argtypes = [c_vp, c_vp, P(ame_dims), c_vp, c_vp]
+    L.ame_sweep.argtypes = [P(ame_dims), P(ame_sweep_args), c_vp]
+    L.ame_sweep_max_slices.argtypes = [ctypes.c_int, ctypes.c_int]
+    L.ame_sweep_lds_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
+    L.ame_sweep_lds_bytes.restype = ctypes.c_longlong
+    L.ame_cov.argtypes = [P(ame_dims), P(ame_cov_args), c_vp]
+    L.ame_elbo.argtypes = [P(ame_dims), P(ame_elbo_args), c_vp]
+    L.ame_elbo_work_size.argtypes = [P(ame_dims)]
+    L.ame_elbo_work_size.restype = ctypes.c_longlong
+    L.ame_supported_r.argtypes = [P(ctypes.c_int), ctypes.c_int]
+    L.ame_last_error.restype = ctypes.c_char_p
+    L.ame_version.restype = ctypes.c_char_p
+    for name in ("ame_pack_y", "ame_sweep", "ame_cov", "ame_elbo", "ame_sweep_max_slices",
+                 "ame_supported_r"):
+        getattr(L, name).restype = ctypes.c_int
+    return L
+
+
+def lib():
+    """Load libame_amd.so (built by ame_amd.build / __graft_entry__.build())."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(
+                    f"ame_amd: HIP library not found at {LIB_PATH}; run "
+                    "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+            try:
+                _lib = _declare(ctypes.CDLL(LIB_PATH))
+            except OSError as e:  # pragma: no cover - depends on the box
+                raise RuntimeError(f"ame_amd: cannot load {LIB_PATH}: {e}") from e
+        return _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().ame_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+
+def supported_r():
+    L = lib()
+    buf = (ctypes.c_int * 64)()
+    k = L.ame_supported_r(buf, 64)
+    return tuple(buf[i] for i in range(min(k, 64)))

@@ -1,0 +1,131 @@
+// extern "C" boundary of libame_amd.so (declared in include/ame_amd.h).
+// Argument validation lives here so a bad call fails loudly with a message
+// instead of faulting on the GPU.
+#include <stdio.h>
+#include <string.h>
+
+#include "ame_common.h"
+
+int ame_sweep_dispatch(const ame_dims*, const ame_sweep_args*, hipStream_t);
+int ame_sweep_blocks_per_cu(int n, int r);
+int ame_cov_dispatch(const ame_dims*, const ame_cov_args*, hipStream_t);
+int ame_elbo_dispatch(const ame_dims*, const ame_elbo_args*, hipStream_t);
+long long ame_elbo_work_doubles(const ame_dims*);
+int ame_pack_dispatch(const float*, float*, const ame_dims*, unsigned long long*, hipStream_t);
+
+static thread_local char g_err[512] = "";
+
+static int fail(const char* fmt, int a = 0, int b = 0) {
+    snprintf(g_err, sizeof(g_err), fmt, a, b);
+    return -1;
+}
+
+static bool r_supported(int r) {
+    switch (r) {
+#define X(RR) \
+    case RR: return true;
+        AME_FOR_EACH_R(X)
+#undef X
+        default: return false;
+    }
+}
+
+static int check_dims(const ame_dims* d) {
+    if (d == nullptr) return fail("ame: dims is NULL");
+    if (d->n < 2) return fail("ame: n must be >= 2 (got %d)", d->n);
+    if (!r_supported(d->r)) return fail("ame: latent_dim r=%d not compiled into this library", d->r);
+    if (d->T_local < 1 || d->T_total < 1) return fail("ame: bad T_local=%d T_total=%d", d->T_local, d->T_total);
+    if (d->t_begin < 0 || d->t_begin + d->T_local > d->T_total)
+        return fail("ame: slice range [%d, +T_local) outside T_total", d->t_begin);
+    if (d->variant < AME_GOOD || d->variant > AME_NAIVE) return fail("ame: bad variant %d", d->variant);
+    return 0;
+}
+
+static int launched(int rc, const char* what) {
+    if (rc == 0) return 0;
+    hipError_t e = hipGetLastError();
+    snprintf(g_err, sizeof(g_err), "ame: %s launch failed (rc=%d, hip=%s)", what, rc,
+             hipGetErrorString(e));
+    return -1;
+}
+
+extern "C" {
+
+const char* ame_last_error(void) { return g_err; }
+
+const char* ame_version(void) { return "ame_amd 0.1 gfx950"; }
+
+int ame_supported_r(int* out, int cap) {
+    int c = 0;
+#define X(RR)                       \
+    if (c < cap && out) out[c] = RR; \
+    ++c;
+    AME_FOR_EACH_R(X)
+#undef X
+    return c;
+}
+
+long long ame_sweep_lds_bytes(int n, int r) {
+    if (!r_supported(r) || n < 1) return 0;
+    return sweep_lds_layout(n, r).total;
+}
+
+int ame_sweep_max_slices(int n, int r) {
+    if (!r_supported(r)) return 0;
+    const long long lds = sweep_lds_layout(n, r).total;
+    if (lds > 163840) return 0;
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    const int per_cu = ame_sweep_blocks_per_cu(n, r);
+    return per_cu * cus;
+}
+
+int ame_pack_y(const float* Y, float* Yt, const ame_dims* dims, unsigned long long* mismatch,
+               void* stream) {
+    if (int e = check_dims(dims)) return e;
+    if (!Y || !Yt) return fail("ame_pack_y: NULL buffer");
+    return launched(ame_pack_dispatch(Y, Yt, dims, mismatch, (hipStream_t)stream), "pack");
+}
+
+int ame_sweep(const ame_dims* dims, const ame_sweep_args* a, void* stream) {
+    if (int e = check_dims(dims)) return e;
+    if (!a || !a->Yt || !a->x_old || !a->x_new || !a->hand || !a->snap || !a->consts || !a->status)
+        return fail("ame_sweep: NULL buffer");
+    if (a->epoch == 0) return fail("ame_sweep: epoch must be >= 1");
+    if (dims->t_begin > 0 && !a->halo_in)
+        return fail("ame_sweep: t_begin=%d > 0 needs halo_in", dims->t_begin);
+    if (dims->t_begin + dims->T_local < dims->T_total && !a->next_old)
+        return fail("ame_sweep: rank does not hold T-1 and next_old is NULL");
+    const long long lds = sweep_lds_layout(dims->n, dims->r).total;
+    if (lds > 163840)
+        return fail("ame_sweep: slice state (n=%d, r=%d) exceeds one workgroup's LDS", dims->n, dims->r);
+    const int maxs = ame_sweep_max_slices(dims->n, dims->r);
+    if (dims->T_local > maxs)
+        return fail("ame_sweep: T_local=%d exceeds co-resident workgroups (%d)", dims->T_local, maxs);
+    return launched(ame_sweep_dispatch(dims, a, (hipStream_t)stream), "sweep");
+}
+
+int ame_cov(const ame_dims* dims, const ame_cov_args* a, void* stream) {
+    if (int e = check_dims(dims)) return e;
+    if (!a || !a->x_old || !a->x_new || !a->cov || !a->consts || !a->cov_terms)
+        return fail("ame_cov: NULL buffer");
+    if (a->update && !a->snap) return fail("ame_cov: update needs snap");
+    return launched(ame_cov_dispatch(dims, a, (hipStream_t)stream), "cov");
+}
+
+long long ame_elbo_work_size(const ame_dims* dims) {
+    if (check_dims(dims)) return -1;
+    return ame_elbo_work_doubles(dims);
+}
+
+int ame_elbo(const ame_dims* dims, const ame_elbo_args* a, void* stream) {
+    if (int e = check_dims(dims)) return e;
+    if (!a || !a->Yt || !a->x || !a->cov_terms || !a->consts || !a->phi || !a->work || !a->out)
+        return fail("ame_elbo: NULL buffer");
+    if (dims->t_begin > 0 && !a->prev_final)
+        return fail("ame_elbo: t_begin=%d > 0 needs prev_final", dims->t_begin);
+    return launched(ame_elbo_dispatch(dims, a, (hipStream_t)stream), "elbo");
+}
+
+}  // extern "C"

@@ -1,0 +1,285 @@
+// K0 (Y relayout) and K2/K3 (ELBO + reconstruction sufficient sums).
+//
+// Reference:
+//   _compute_expected_log_likelihood  structured_mf.py:124-150 (naive_mf.py:114-132)
+//   StaticAMEModel.compute_mean        static_ame.py:189-238
+//   _compute_log_prior_initial         structured_mf.py:152-173
+//   _compute_log_prior_transitions     structured_mf.py:175-200
+//   compute_temporal_reconstruction_error  temporal_ame.py:255-291
+//
+// K2 walks 64x64 (i-block, j-block) tiles of one time slice.  The plug-in mean
+// m_ij = [a_i + b_j + U_i.V_j, a_j + b_i + U_j.V_i] needs G1 = U_I V_J^T and
+// G2^T = V_I U_J^T on the same (i,j) -> one f32 MFMA (v_mfma_f32_16x16x4_f32,
+// exact f32) chain each per 16x16 sub-tile, so both land in the same lane and
+// register.  The residual quadratic form and squared error are fused into the
+// epilogue while the tile's Y bytes stream in once.  When Y is swap-consistent
+// (Y_ji = swap(Y_ij), checked by K0) only the upper-triangle tiles are read and
+// the mirror half of the reconstruction error is counted twice.
+#include "ame_common.h"
+
+// ---------------------------------------------------------------------------
+// K0: Y [n][n][T_total][2] -> Yt [T_local][n][n][2]; count swap mismatches.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(AME_NT)
+ame_pack_kernel(const float* __restrict__ Y, float* __restrict__ Yt, ame_dims dm,
+                unsigned long long* mismatch) {
+    const int n = dm.n, TL = dm.T_local, Tt = dm.T_total;
+    const size_t total = (size_t)TL * n * n;
+    unsigned long long bad = 0;
+    for (size_t idx = (size_t)blockIdx.x * AME_NT + threadIdx.x; idx < total;
+         idx += (size_t)gridDim.x * AME_NT) {
+        const int j = (int)(idx % n);
+        const size_t r = idx / n;
+        const int i = (int)(r % n);
+        const int tl = (int)(r / n);
+        const int tg = dm.t_begin + tl;
+        const float2 y = *(const float2*)(Y + (((size_t)i * n + j) * Tt + tg) * 2);
+        *(float2*)(Yt + idx * 2) = y;
+        if (i < j && mismatch != nullptr) {
+            const float2 yt = *(const float2*)(Y + (((size_t)j * n + i) * Tt + tg) * 2);
+            if (__float_as_uint(yt.x) != __float_as_uint(y.y) ||
+                __float_as_uint(yt.y) != __float_as_uint(y.x))
+                ++bad;
+        }
+    }
+    if (mismatch != nullptr && bad) atomicAdd(mismatch, bad);
+}
+
+int ame_pack_dispatch(const float* Y, float* Yt, const ame_dims* dm, unsigned long long* mm,
+                      hipStream_t st) {
+    const size_t total = (size_t)dm->T_local * dm->n * dm->n;
+    size_t blocks = (total + AME_NT - 1) / AME_NT;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(ame_pack_kernel, dim3((unsigned)blocks), dim3(AME_NT), 0, st, Y, Yt, *dm,
+                       mm);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// ---------------------------------------------------------------------------
+// K2: pair terms.  work layout: [nwg2][2] = {sum quad (i<j), sum sq-err}
+// ---------------------------------------------------------------------------
+#define AME_TILE 64
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int R>
+__global__ void __launch_bounds__(AME_NT)
+ame_pairs_kernel(ame_dims dm, const float* __restrict__ Yt, const float* __restrict__ x,
+                 double r00, double r01, double r10, double r11, int swap_mode,
+                 double* __restrict__ partial) {
+    constexpr int D = 2 + 2 * R;
+    constexpr int RP = (R + 3) & ~3;   // MFMA K padded to 4
+    constexpr int LD = RP + 1;         // LDS row stride (bank spread)
+    const int n = dm.n;
+    const int nb = (n + AME_TILE - 1) / AME_TILE;
+    const int ntile = swap_mode ? nb * (nb + 1) / 2 : nb * nb;
+    const int tl = blockIdx.x / ntile;
+    int tix = blockIdx.x - tl * ntile;
+    int I, J;
+    if (swap_mode) {   // upper-triangle tile enumeration, row-major
+        I = 0;
+        while (tix >= nb - I) { tix -= nb - I; ++I; }
+        J = I + tix;
+    } else {
+        I = tix / nb;
+        J = tix - I * nb;
+    }
+    const int I0 = I * AME_TILE, J0 = J * AME_TILE;
+
+    __shared__ float UI[AME_TILE * LD], VI[AME_TILE * LD], UJ[AME_TILE * LD], VJ[AME_TILE * LD];
+    __shared__ float aI[AME_TILE], bI[AME_TILE], aJ[AME_TILE], bJ[AME_TILE];
+    __shared__ double red[8];
+
+    const float* xs = x + (size_t)tl * n * D;
+    for (int idx = threadIdx.x; idx < AME_TILE * RP; idx += AME_NT) {
+        const int row = idx / RP, k = idx - row * RP;
+        const int ii = I0 + row, jj = J0 + row;
+        const bool kin = k < R;
+        UI[row * LD + k] = (kin && ii < n) ? xs[(size_t)ii * D + 2 + k] : 0.f;
+        VI[row * LD + k] = (kin && ii < n) ? xs[(size_t)ii * D + 2 + R + k] : 0.f;
+        UJ[row * LD + k] = (kin && jj < n) ? xs[(size_t)jj * D + 2 + k] : 0.f;
+        VJ[row * LD + k] = (kin && jj < n) ? xs[(size_t)jj * D + 2 + R + k] : 0.f;
+    }
+    if (threadIdx.x < AME_TILE) {
+        const int row = threadIdx.x;
+        const int ii = I0 + row, jj = J0 + row;
+        aI[row] = ii < n ? xs[(size_t)ii * D + 0] : 0.f;
+        bI[row] = ii < n ? xs[(size_t)ii * D + 1] : 0.f;
+        aJ[row] = jj < n ? xs[(size_t)jj * D + 0] : 0.f;
+        bJ[row] = jj < n ? xs[(size_t)jj * D + 1] : 0.f;
+    }
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int qi = w >> 1, qj = w & 1;
+    const int lr = lane & 15, lk = lane >> 4;
+    const float p = (float)r00, q01 = (float)r01, q10 = (float)r10, s = (float)r11;
+    const float* ys = Yt + (size_t)tl * n * n * 2;
+    double quad = 0.0, sq = 0.0;
+#pragma unroll
+    for (int si = 0; si < 2; ++si) {
+#pragma unroll
+        for (int sj = 0; sj < 2; ++sj) {
+            const int ii0 = qi * 32 + si * 16, jj0 = qj * 32 + sj * 16;
+            f32x4 g1 = {0.f, 0.f, 0.f, 0.f}, g2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k0 = 0; k0 < RP; k0 += 4) {
+                const float a1 = UI[(ii0 + lr) * LD + k0 + lk];
+                const float b1 = VJ[(jj0 + lr) * LD + k0 + lk];
+                g1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, g1, 0, 0, 0);
+                const float a2 = VI[(ii0 + lr) * LD + k0 + lk];
+                const float b2 = UJ[(jj0 + lr) * LD + k0 + lk];
+                g2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a2, b2, g2, 0, 0, 0);
+            }
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const int ii = ii0 + lk * 4 + v, jj = jj0 + lr;
+                const int i = I0 + ii, j = J0 + jj;
+                if (i >= n || j >= n || i == j) continue;
+                if (swap_mode && i > j) continue;
+                const float2 y = *(const float2*)(ys + ((size_t)i * n + j) * 2);
+                const float mu0 = (aI[ii] + bJ[jj]) + g1[v];
+                const float mu1 = (aJ[jj] + bI[ii]) + g2[v];
+                const float e0 = y.x - mu0, e1 = y.y - mu1;
+                const float se = e0 * e0 + e1 * e1;
+                if (i < j) {
+                    quad += (double)(e0 * (p * e0 + q01 * e1) + e1 * (q10 * e0 + s * e1));
+                    sq += swap_mode ? 2.0 * (double)se : (double)se;
+                } else {
+                    sq += (double)se;
+                }
+            }
+        }
+    }
+    double v2[2] = {quad, sq};
+    block_sum<2>(v2, red);
+    if (threadIdx.x == 0) {
+        partial[(size_t)blockIdx.x * 2 + 0] = v2[0];
+        partial[(size_t)blockIdx.x * 2 + 1] = v2[1];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K3: per-(node, slice) terms.  partial3 layout [nwg3][6]:
+//   {mu0' S0i mu0, tr(S0i S_0), e' Qi e (t>=1), tr(Qi S) (t>=1), logdet S, tr S}
+// ---------------------------------------------------------------------------
+template <int R>
+__global__ void __launch_bounds__(AME_NT)
+ame_nodes_kernel(ame_dims dm, const float* __restrict__ x, const float* __restrict__ prev_final,
+                 const double* __restrict__ cov_terms, const double* __restrict__ consts,
+                 const double* __restrict__ phi, double* __restrict__ partial) {
+    constexpr int D = 2 + 2 * R;
+    const int n = dm.n;
+    const size_t DD = (size_t)D * D;
+    __shared__ double red[4 * 6];
+    const int idx = blockIdx.x * AME_NT + threadIdx.x;
+    double v[6] = {0, 0, 0, 0, 0, 0};
+    if (idx < dm.T_local * n) {
+        const int tl = idx / n, i = idx - tl * n;
+        const int tg = dm.t_begin + tl;
+        const float* mu = x + ((size_t)tl * n + i) * D;
+        const double* ct = cov_terms + ((size_t)tl * n + i) * 4;
+        v[4] = ct[0];
+        v[5] = ct[1];
+        if (tg == 0) {
+            double qsum = 0.0;
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                double row = 0.0;
+#pragma unroll
+                for (int m = 0; m < D; ++m) row = fma(consts[(size_t)k * D + m], (double)mu[m], row);
+                qsum = fma((double)mu[k], row, qsum);
+            }
+            v[0] = qsum;
+            v[1] = ct[3];
+        } else {
+            const float* pr = (tl > 0) ? x + ((size_t)(tl - 1) * n + i) * D : prev_final + (size_t)i * D;
+            double e[D];
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                double pm = 0.0;
+#pragma unroll
+                for (int m = 0; m < D; ++m) pm = fma(phi[(size_t)k * D + m], (double)pr[m], pm);
+                e[k] = (double)mu[k] - pm;
+            }
+            double qsum = 0.0;
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                double row = 0.0;
+#pragma unroll
+                for (int m = 0; m < D; ++m) row = fma(consts[DD + (size_t)k * D + m], e[m], row);
+                qsum = fma(e[k], row, qsum);
+            }
+            v[2] = qsum;
+            v[3] = ct[2];
+        }
+    }
+    block_sum<6>(v, red);
+    if (threadIdx.x == 0)
+        for (int q = 0; q < 6; ++q) partial[(size_t)blockIdx.x * 6 + q] = v[q];
+}
+
+// Final deterministic reduction -> out[8]
+__global__ void __launch_bounds__(AME_NT)
+ame_final_kernel(const double* __restrict__ p2, int n2, const double* __restrict__ p3, int n3,
+                 double* __restrict__ out) {
+    __shared__ double red[4 * 8];
+    double v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int b = threadIdx.x; b < n2; b += AME_NT) {
+        v[0] += p2[(size_t)b * 2 + 0];
+        v[7] += p2[(size_t)b * 2 + 1];
+    }
+    for (int b = threadIdx.x; b < n3; b += AME_NT) {
+        const double* r = p3 + (size_t)b * 6;
+        v[2] += r[0];
+        v[3] += r[1];
+        v[4] += r[2];
+        v[5] += r[3];
+        v[6] += r[4];
+        v[1] += r[5];
+    }
+    block_sum<8>(v, red);
+    if (threadIdx.x == 0)
+        for (int q = 0; q < 8; ++q) out[q] = v[q];
+}
+
+static inline long long pairs_blocks(const ame_dims* dm, int swap_mode) {
+    const long long nb = (dm->n + AME_TILE - 1) / AME_TILE;
+    return (long long)dm->T_local * (swap_mode ? nb * (nb + 1) / 2 : nb * nb);
+}
+static inline long long nodes_blocks(const ame_dims* dm) {
+    return ((long long)dm->T_local * dm->n + AME_NT - 1) / AME_NT;
+}
+
+long long ame_elbo_work_doubles(const ame_dims* dm) {
+    return 2 * pairs_blocks(dm, 0) + 6 * nodes_blocks(dm) + 16;
+}
+
+template <int R>
+static int launch_elbo(const ame_dims* dm, const ame_elbo_args* a, hipStream_t st) {
+    const long long b2 = pairs_blocks(dm, a->swap_consistent);
+    const long long b3 = nodes_blocks(dm);
+    double* p2 = a->work;
+    double* p3 = a->work + 2 * b2;
+    if (b2 > 0)
+        hipLaunchKernelGGL(ame_pairs_kernel<R>, dim3((unsigned)b2), dim3(AME_NT), 0, st, *dm, a->Yt,
+                           a->x, a->rinv[0], a->rinv[1], a->rinv[2], a->rinv[3],
+                           a->swap_consistent, p2);
+    if (b3 > 0)
+        hipLaunchKernelGGL(ame_nodes_kernel<R>, dim3((unsigned)b3), dim3(AME_NT), 0, st, *dm, a->x,
+                           a->prev_final, a->cov_terms, a->consts, a->phi, p3);
+    hipLaunchKernelGGL(ame_final_kernel, dim3(1), dim3(AME_NT), 0, st, p2, (int)b2, p3, (int)b3,
+                       a->out);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+int ame_elbo_dispatch(const ame_dims* dm, const ame_elbo_args* a, hipStream_t st) {
+    switch (dm->r) {
+#define X(RR) \
+    case RR: return launch_elbo<RR>(dm, a, st);
+        AME_FOR_EACH_R(X)
+#undef X
+        default: return -1;
+    }
+}

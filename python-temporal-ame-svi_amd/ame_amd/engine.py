@@ -1,0 +1,281 @@
+"""Device engine: HBM-resident VI state + the per-iteration kernel sequence.
+
+One engine per process / GPU.  It owns, for the local time slices
+[t_begin, t_begin + T_local):
+
+    Yt        [T_local][n][n][2] fp32   observed network, time-major (ame_pack_y)
+    x_a, x_b  [T_local][n][d]    fp32   means, ping-pong (old / new of a sweep)
+    cov       [T_local][n][d][d] fp32   covariances, updated in place
+    hand      [T_local][n][d]    u64    lane-to-lane {epoch,value} granules
+    snap      [T_local][n/16][2r+3r^2] fp64 sweep statistic snapshots
+    cov_terms [T_local][n][4]    fp64   per-(node,time) covariance ELBO terms
+
+and runs, per fit() iteration (reference base.py:170-181):
+
+    ame_sweep   (means; _update_step)       structured_mf.py:211-326
+    ame_cov     (covariances + cov terms)   structured_mf.py:266-287, 202-209
+    ame_elbo    (pair + node sums)          structured_mf.py:115-200, temporal_ame.py:255-291
+
+The host then assembles ELBO and MSE from 8 fp64 sums (+ the analytic
+constants) exactly as the reference's formulas define them.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from . import _lib
+
+LOG2PI = math.log(2.0 * math.pi)
+SNAP_NB = 16
+VARIANTS = {"good": _lib.AME_GOOD, "bad": _lib.AME_BAD, "naive": _lib.AME_NAIVE}
+
+
+@dataclass
+class Shard:
+    """Contiguous block of time slices held by this rank."""
+    t_begin: int
+    T_local: int
+    T_total: int
+    rank: int = 0
+    world: int = 1
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _blockdiag(Sigma, Psi):
+    d = 2 + Psi.shape[0]
+    S = torch.zeros(d, d, dtype=torch.float64)
+    S[:2, :2] = Sigma.double()
+    S[2:, 2:] = Psi.double()
+    return S
+
+
+def _sym(a):
+    return 0.5 * (a + a.T)
+
+
+class Constants:
+    """fp64 model constants, built from the fp32 model attributes the reference reads."""
+
+    def __init__(self, model):
+        d = model.d
+        self.R = model.R.detach().double().cpu()
+        self.R_inv = model.R_inv.detach().double().cpu()
+        S0 = _blockdiag(model.Sigma.detach().cpu(), model.Psi.detach().cpu())
+        Q = model.Q.detach().double().cpu()
+        Phi = model.Phi.detach().double().cpu()
+        self.S0inv = _sym(torch.linalg.inv(S0))
+        self.Qinv = _sym(torch.linalg.inv(Q))
+        self.PtQiP = _sym(Phi.T @ self.Qinv @ Phi)
+        self.QiPhi = self.Qinv @ Phi
+        self.PhiTQi = Phi.T @ self.Qinv
+        self.Phi = Phi
+        self.logdetR = float(torch.logdet(self.R))
+        self.trRinv = float(torch.trace(self.R_inv))
+        self.logdetS0 = float(torch.logdet(S0))
+        self.logdetQ = float(torch.logdet(Q))
+        self.stack = torch.stack([self.S0inv, self.Qinv, self.PtQiP, self.QiPhi,
+                                  self.PhiTQi]).contiguous()
+        self.d = d
+
+    def rinv4(self):
+        r = self.R_inv.flatten().tolist()
+        return (ctypes.c_double * 4)(*r)
+
+
+def assemble(out, n, T, d, variant, C: Constants):
+    """ELBO pieces and MSE from the 8 device sums (see include/ame_amd.h).
+
+    Formulas: structured_mf.py:124-209 / naive_mf.py:114-191 and
+    temporal_ame.py:290 with the pairwise correction collapsed as
+    sum_{i<j}(tr_i + tr_j) = (n-1) sum_i tr_i.
+    """
+    npairs = T * n * (n - 1) / 2.0
+    corr = 0.0 if variant == "naive" else 0.1 * C.trRinv / d * (n - 1) * out[1]
+    loglik = -0.5 * (npairs * (C.logdetR + 2 * LOG2PI) + out[0] + corr)
+    prior0 = -0.5 * (n * (C.logdetS0 + d * LOG2PI) + out[2] + out[3])
+    trans = -0.5 * (n * (T - 1) * (C.logdetQ + d * LOG2PI) + out[4] + out[5])
+    ent = 0.5 * (n * T * d * (1 + LOG2PI) + out[6])
+    recon = out[7] / (n * (n - 1) * T)
+    return {"loglik": loglik, "prior0": prior0, "trans": trans, "entropy": ent,
+            "elbo": loglik + prior0 + trans + ent, "recon": recon}
+
+
+class DeviceEngine:
+    """HBM-resident state of one VI run on one GPU (one time shard)."""
+
+    def __init__(self, model, variant: str, lr: float, X_mean: torch.Tensor,
+                 X_cov: torch.Tensor, device=None, shard: Optional[Shard] = None,
+                 halo=None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("ame_amd: no GPU visible; the HIP path has no CPU fallback")
+        self.L = _lib.lib()
+        if variant not in VARIANTS:
+            raise ValueError(f"Unknown factorization '{variant}'")
+        self.variant = variant
+        self.vcode = VARIANTS[variant]
+        self.n, self.T, self.d, self.r = int(model.n), int(model.T), int(model.d), int(model.r)
+        if self.r not in _lib.supported_r():
+            raise RuntimeError(f"ame_amd: latent_dim={self.r} not compiled "
+                               f"(supported {_lib.supported_r()})")
+        self.dev = torch.device(device) if device is not None else torch.device(
+            "cuda", torch.cuda.current_device())
+        self.shard = shard or Shard(0, self.T, self.T)
+        self.halo = halo
+        self.lr = float(lr)
+        self.C = Constants(model)
+        sh = self.shard
+        self.dims = _lib.ame_dims(self.n, self.r, sh.T_local, sh.t_begin, sh.T_total, self.vcode)
+        dev = self.dev
+        with torch.cuda.device(dev):
+            self.stream = torch.cuda.current_stream(dev)
+            self.consts = self.C.stack.to(dev)
+            self.phi = self.C.Phi.contiguous().to(dev)
+            self._pack_y(model.Y)
+            t0, t1 = sh.t_begin, sh.t_begin + sh.T_local
+            self.x_a = X_mean[:, t0:t1].detach().float().permute(1, 0, 2).contiguous().to(dev)
+            self.x_b = torch.empty_like(self.x_a)
+            self.cov = X_cov[:, t0:t1].detach().float().permute(1, 0, 2, 3).contiguous().to(dev)
+            n, d, TL = self.n, self.d, sh.T_local
+            nblk = (n + SNAP_NB - 1) // SNAP_NB
+            ns = 2 * self.r + 3 * self.r * self.r
+            self.hand = torch.zeros(TL * n * d, dtype=torch.int64, device=dev)
+            self.snap = torch.empty(TL * nblk * ns, dtype=torch.float64, device=dev)
+            self.cov_terms = torch.zeros(TL * n * 4, dtype=torch.float64, device=dev)
+            ws = int(self.L.ame_elbo_work_size(ctypes.byref(self.dims)))
+            if ws < 0:
+                _lib.check(-1, "ame_elbo_work_size")
+            self.work = torch.empty(ws, dtype=torch.float64, device=dev)
+            self.out = torch.zeros(8, dtype=torch.float64, device=dev)
+            self.status = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.epoch = 0
+        self.max_slices = int(self.L.ame_sweep_max_slices(self.n, self.r))
+        if sh.T_local > self.max_slices:
+            raise RuntimeError(
+                f"ame_amd: {sh.T_local} time slices per GPU exceed the co-resident sweep "
+                f"lanes ({self.max_slices}) for n={self.n}, r={self.r}; shard over more GPUs")
+        self._out_host = None
+        self._out_valid = False
+
+    # ------------------------------------------------------------------
+    def _sp(self):
+        return ctypes.c_void_p(self.stream.cuda_stream)
+
+    def _pack_y(self, Y):
+        if Y is None:
+            raise ValueError("No data generated yet. Call generate_data() first.")
+        sh = self.shard
+        src = Y.detach()
+        if src.dtype != torch.float32:
+            src = src.float()
+        src = src.to(self.dev).contiguous()
+        self.Yt = torch.empty(sh.T_local, self.n, self.n, 2, dtype=torch.float32, device=self.dev)
+        mm = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        rc = self.L.ame_pack_y(_ptr(src), _ptr(self.Yt), ctypes.byref(self.dims), _ptr(mm),
+                               self._sp())
+        _lib.check(rc, "ame_pack_y")
+        self.swap_consistent = int(mm.item()) == 0
+        del src
+
+    # ------------------------------------------------------------------
+    def sweep(self):
+        """One Gauss-Seidel sweep + covariance update (reference _update_step)."""
+        sh = self.shard
+        self.epoch += 1
+        halo_in = halo_out = next_old = None
+        if self.halo is not None:
+            next_old, halo_in, halo_out = self.halo.before_sweep(self)
+        a = _lib.ame_sweep_args(
+            Yt=_ptr(self.Yt), x_old=_ptr(self.x_a), x_new=_ptr(self.x_b), next_old=next_old,
+            hand=_ptr(self.hand), halo_in=halo_in, halo_out=halo_out, snap=_ptr(self.snap),
+            consts=_ptr(self.consts), rinv=self.C.rinv4(), lr=self.lr,
+            one_minus_lr=float(1.0 - self.lr), epoch=self.epoch, status=_ptr(self.status))
+        _lib.check(self.L.ame_sweep(ctypes.byref(self.dims), ctypes.byref(a), self._sp()),
+                   "ame_sweep")
+        c = _lib.ame_cov_args(
+            x_old=_ptr(self.x_a), x_new=_ptr(self.x_b), cov=_ptr(self.cov), snap=_ptr(self.snap),
+            consts=_ptr(self.consts), cov_terms=_ptr(self.cov_terms), rinv=self.C.rinv4(),
+            lr=self.lr, one_minus_lr=float(1.0 - self.lr), update=1)
+        _lib.check(self.L.ame_cov(ctypes.byref(self.dims), ctypes.byref(c), self._sp()), "ame_cov")
+        self.x_a, self.x_b = self.x_b, self.x_a
+        self._out_valid = False
+        self._cov_terms_valid = True
+        if self.halo is not None:
+            self.halo.after_sweep(self)
+
+    def refresh_cov_terms(self):
+        """Covariance ELBO terms of the current covariances (no update)."""
+        c = _lib.ame_cov_args(
+            x_old=_ptr(self.x_a), x_new=_ptr(self.x_a), cov=_ptr(self.cov), snap=None,
+            consts=_ptr(self.consts), cov_terms=_ptr(self.cov_terms), rinv=self.C.rinv4(),
+            lr=self.lr, one_minus_lr=float(1.0 - self.lr), update=0)
+        _lib.check(self.L.ame_cov(ctypes.byref(self.dims), ctypes.byref(c), self._sp()), "ame_cov")
+        self._cov_terms_valid = True
+
+    def launch_elbo(self):
+        if not getattr(self, "_cov_terms_valid", False):
+            self.refresh_cov_terms()
+        prev_final = None
+        if self.halo is not None:
+            prev_final = self.halo.prev_final(self)
+        e = _lib.ame_elbo_args(
+            Yt=_ptr(self.Yt), x=_ptr(self.x_a), prev_final=prev_final,
+            cov_terms=_ptr(self.cov_terms), consts=_ptr(self.consts), phi=_ptr(self.phi),
+            rinv=self.C.rinv4(), swap_consistent=1 if self.swap_consistent else 0,
+            work=_ptr(self.work), out=_ptr(self.out))
+        _lib.check(self.L.ame_elbo(ctypes.byref(self.dims), ctypes.byref(e), self._sp()),
+                   "ame_elbo")
+
+    def sums(self):
+        """The 8 fp64 sums for the current state (all ranks reduced)."""
+        if not self._out_valid:
+            self.launch_elbo()
+            out = self.out
+            if self.halo is not None:
+                out = self.halo.allreduce_sums(out)
+            self._out_host = out.cpu().tolist()
+            self._check_status()
+            self._out_valid = True
+        return self._out_host
+
+    def terms(self):
+        return assemble(self.sums(), self.n, self.T, self.d, self.variant, self.C)
+
+    def _check_status(self):
+        st = int(self.status.item())
+        if st:
+            self.status.zero_()
+            raise RuntimeError(f"ame_amd: sweep reported device status {st:#x} "
+                               "(hand-off spin timed out: lanes not co-resident?)")
+
+    def invalidate(self):
+        self._out_valid = False
+        self._cov_terms_valid = False
+
+    # ------------------------------------------------------------------
+    # state transfer (reference layout (n, T, d[, d]))
+    # ------------------------------------------------------------------
+    def means_local(self) -> torch.Tensor:
+        return self.x_a.permute(1, 0, 2)
+
+    def covs_local(self) -> torch.Tensor:
+        return self.cov.permute(1, 0, 2, 3)
+
+    def set_means(self, X_mean: torch.Tensor):
+        sh = self.shard
+        t0, t1 = sh.t_begin, sh.t_begin + sh.T_local
+        self.x_a.copy_(X_mean[:, t0:t1].detach().float().permute(1, 0, 2))
+        self.invalidate()
+
+    def set_covs(self, X_cov: torch.Tensor):
+        sh = self.shard
+        t0, t1 = sh.t_begin, sh.t_begin + sh.T_local
+        self.cov.copy_(X_cov[:, t0:t1].detach().float().permute(1, 0, 2, 3))
+        self.invalidate()

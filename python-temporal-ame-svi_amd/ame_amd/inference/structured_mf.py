@@ -1,0 +1,67 @@
+"""Structured mean-field VI for temporal AME on MI355X.
+
+Drop-in for the reference ``TemporalAMEStructuredMFVI``
+(src/inference/structured_mf.py:28-338): same constructor arguments, same
+initialisation random stream, same ``fit`` / getters / ``history`` semantics.
+The per-iteration work (sweep, covariance update, ELBO, reconstruction error)
+runs as hand-written gfx950 kernels through libame_amd.so (include/ame_amd.h).
+"""
+from __future__ import annotations
+
+from typing import Literal
+
+import torch
+
+from ._device_vi import DeviceTemporalVI
+
+
+class TemporalAMEStructuredMFVI(DeviceTemporalVI):
+    """Parameters follow structured_mf.py:58-72.  Extra (build-only) keyword
+    arguments: ``device`` (default: current / LOCAL_RANK GPU) and
+    ``distributed`` (None = time-shard automatically when torch.distributed is
+    initialised with world_size > 1)."""
+
+    def __init__(self, model, factorization: Literal["good", "bad"] = "good",
+                 learning_rate: float = 1.0, init_scale: float = 0.1,
+                 cov_init_scale: float = 0.5, seed: int = 42, device=None, distributed=None):
+        self.factorization = factorization
+        self.init_scale = init_scale
+        self.cov_init_scale = cov_init_scale
+        self._variant = factorization
+        super().__init__(model, learning_rate, seed, device=device, distributed=distributed)
+
+    def _initialize_variational_params(self) -> None:
+        """structured_mf.py:74-113: identical random stream (one randn(n,T,d),
+        then one randn per block per (i,t), in loop order); the elementwise
+        arithmetic is batched, which is bit-identical in fp32."""
+        n, T, d, r = self.n, self.T, self.d, self.r
+        self.X_mean = torch.randn(n, T, d) * self.init_scale
+        if self.factorization == "good":
+            E = torch.stack([torch.randn(d, d) for _ in range(n * T)]).view(n, T, d, d)
+            eye = torch.eye(d)
+            cov = eye * self.cov_init_scale
+            cov = cov + E * 0.01
+            cov = (cov + cov.transpose(-1, -2)) / 2
+            cov = cov + eye * 0.1
+            self.X_cov = cov.contiguous()
+        elif self.factorization == "bad":
+            r2 = 2 * r
+            E1 = torch.empty(n * T, 2, 2)
+            E2 = torch.empty(n * T, r2, r2)
+            for k in range(n * T):
+                E1[k] = torch.randn(2, 2)
+                E2[k] = torch.randn(r2, r2)
+            b1 = torch.eye(2) * self.cov_init_scale + E1 * 0.01
+            b1 = (b1 + b1.transpose(-1, -2)) / 2 + torch.eye(2) * 0.05
+            b2 = torch.eye(r2) * self.cov_init_scale + E2 * 0.01
+            b2 = (b2 + b2.transpose(-1, -2)) / 2 + torch.eye(r2) * 0.05
+            cov = torch.zeros(n * T, d, d)
+            cov[:, :2, :2] = b1
+            cov[:, 2:, 2:] = b2
+            self.X_cov = cov.view(n, T, d, d).contiguous()
+        else:
+            self.X_cov = torch.zeros(n, T, d, d)
+            raise ValueError(f"Unknown factorization '{self.factorization}'")
+
+    def get_factorization_type(self) -> str:
+        return self.factorization

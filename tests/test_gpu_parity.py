@@ -1,0 +1,182 @@
+"""GPU parity: the HIP path (libame_amd.so) against the reference's own outputs
+(golden fixtures captured by tests/golden/make_golden.py) and against the CPU
+oracle (oracle/ame_oracle.py).
+
+Tolerances (stated here):
+  * vs fp64 reference / fp64 oracle: ELBO and MSE relative 2e-6, means
+    absolute 2e-6 * max(1, max|mu|), covariances absolute 1e-6 * max(1, max|S|).
+    The device keeps means/covariances in fp32 storage and solves in fp64, so
+    this is fp32 storage rounding amplified over a few iterations.
+  * vs fp32 reference: 10x looser (the fp32 reference itself differs from the
+    fp64 reference by up to 1.6e-5 on the means at n=40, lr=1).
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, golden, golden_params
+
+pytestmark = pytest.mark.gpu
+
+CFG = {"c1": (15, 10, 2), "tfix": (10, 5, 2), "mid": (40, 12, 3)}
+
+
+def _make(tag):
+    from ame_amd import TemporalAMEModel
+    n, T, r = CFG[tag]
+    m = TemporalAMEModel(n, T, r, ar_coefficient=0.8, rho_dyadic=0.5, seed=42)
+    m.generate_data()
+    return m
+
+
+def _vi(model, method, lr, dev):
+    from ame_amd import TemporalAMENaiveMFVI, TemporalAMEStructuredMFVI
+    if method == "naive":
+        return TemporalAMENaiveMFVI(model, learning_rate=lr, device=dev)
+    return TemporalAMEStructuredMFVI(model, factorization=method, learning_rate=lr, device=dev)
+
+
+def _fixtures():
+    out = []
+    for f in sorted(glob.glob(os.path.join(GOLDEN, "*_lr*.npz"))):
+        name = os.path.basename(f)
+        if name.endswith("_f64.npz"):
+            continue
+        tag, method = name.split("_")[:2]
+        lr = float(name.split("_lr")[1].replace(".npz", ""))
+        out.append((tag, method, lr, name))
+    return out
+
+
+@pytest.mark.parametrize("tag,method,lr,name", _fixtures())
+def test_golden_trajectory(tag, method, lr, name, gpu_device):
+    z32 = golden(name)
+    f64 = name.replace(".npz", "_f64.npz")
+    z = golden(f64) if os.path.exists(os.path.join(GOLDEN, f64)) else z32
+    k = 1.0 if z is not z32 else 10.0
+    m = _make(tag)
+    vi = _vi(m, method, lr, gpu_device)
+    assert np.array_equal(vi.X_mean.numpy(), z32["init_mean"])
+    assert np.array_equal(vi.X_cov.numpy(), z32["init_cov"])
+    iters = int(z["iters"])
+    for it in range(1, iters + 1):
+        vi.fit(max_iter=1, tolerance=0.0, verbose=False)
+        if f"mean_{it}" in z:
+            ref = z[f"mean_{it}"]
+            err = np.abs(vi.X_mean.numpy().astype(np.float64) - ref).max()
+            assert err <= k * 2e-6 * max(1.0, np.abs(ref).max()), (it, err)
+        if f"cov_{it}" in z:
+            ref = z[f"cov_{it}"]
+            err = np.abs(vi.X_cov.numpy().astype(np.float64) - ref).max()
+            assert err <= k * 1e-6 * max(1.0, np.abs(ref).max()), (it, err)
+    e = np.array([float(x) for x in vi.history["elbo"]])
+    rec = np.array(vi.history["reconstruction_error"])
+    assert np.all(np.abs(e - z["elbo"]) <= k * 2e-6 * np.abs(z["elbo"])), (e, z["elbo"])
+    assert np.all(np.abs(rec - z["recon"]) <= k * 2e-6 * np.abs(z["recon"])), (rec, z["recon"])
+    sp = vi.elbo_terms()
+    got = np.array([sp["loglik"], sp["prior0"], sp["trans"], sp["entropy"]])
+    ref = z["elbo_split"][-1]
+    assert np.all(np.abs(got - ref) <= k * 2e-6 * np.abs(z["elbo"][-1])), (got, ref)
+
+
+def test_demo_100_iterations(gpu_device):
+    """demo.py settings (lr=0.01, 100 iterations) for all three methods."""
+    z = golden("c1_demo100.npz")
+    for method in ("good", "bad", "naive"):
+        m = _make("c1")
+        vi = _vi(m, method, 0.01, gpu_device)
+        h = vi.fit(max_iter=100, verbose=False)
+        e = np.array([float(x) for x in h["elbo"]])
+        ref = z[f"{method}_elbo"]
+        assert len(e) == len(ref)
+        assert np.all(np.abs(e - ref) <= 2e-5 * np.abs(ref)), method
+        assert np.allclose(h["reconstruction_error"], z[f"{method}_recon"], rtol=2e-5, atol=0)
+        assert np.abs(vi.X_mean.numpy() - z[f"{method}_mean"]).max() < 2e-4
+
+
+def test_single_node_update(gpu_device):
+    """Observation terms / one node update at init (structured_mf.py:289-326)."""
+    z = golden("c1_single_step.npz")
+    import ame_oracle as O
+    P = golden_params("c1")
+    m = _make("c1")
+    Y = m.Y.numpy().astype(np.float64)
+    for method in ("good", "bad"):
+        Xm = z[f"{method}_before_mean"].astype(np.float64)
+        for (i, t), Pr, hr in zip(z[f"{method}_obs_it"], z[f"{method}_obs_P"], z[f"{method}_obs_h"]):
+            Po, ho = O.observation_terms(Y, Xm, P["R_inv"], int(i), int(t))
+            assert np.allclose(Po, Pr, rtol=1e-5, atol=1e-4)
+            assert np.allclose(ho, hr, rtol=1e-5, atol=1e-4)
+    # one full sweep on the GPU: node 0 must equal the reference's _update_node_i(0)
+    for method in ("good", "bad"):
+        vi = _vi(_make("c1"), method, 1.0, gpu_device)
+        vi.fit(max_iter=1, tolerance=0.0, verbose=False)
+        ref = z[f"{method}_after0_mean"][0]
+        assert np.abs(vi.X_mean.numpy()[0] - ref).max() < 2e-5
+
+
+@pytest.mark.parametrize("n,T,r,method,lr", [
+    (33, 7, 1, "good", 0.5), (64, 16, 4, "good", 0.01), (50, 9, 5, "bad", 1.0),
+    (48, 6, 8, "naive", 0.3), (70, 5, 6, "good", 1.0), (40, 4, 16, "good", 0.01),
+    (20, 1, 2, "good", 1.0), (2, 3, 2, "bad", 0.7), (24, 3, 7, "naive", 1.0)])
+def test_vs_oracle_fp64(n, T, r, method, lr, gpu_device):
+    """Random configurations (odd r, T=1, n=2, ...) against the fp64 oracle."""
+    import ame_oracle as O
+    from ame_amd import TemporalAMEModel
+    m = TemporalAMEModel(n, T, r, seed=7)
+    m.generate_data_fast(seed=11)
+    vi = _vi(m, method, lr, gpu_device)
+    Xm = vi.X_mean.numpy().astype(np.float64).copy()
+    Xc = vi.X_cov.numpy().astype(np.float64).copy()
+    params = {k: getattr(m, k).numpy().astype(np.float64)
+              for k in ("R", "R_inv", "Sigma", "Psi", "Phi", "Q")}
+    Y = m.Y.numpy().astype(np.float64)
+    ref = O.fit(Y, Xm, Xc, params, method, lr, max_iter=2, tolerance=0.0)
+    h = vi.fit(max_iter=2, tolerance=0.0, verbose=False)
+    err = np.abs(vi.X_mean.numpy() - Xm).max()
+    assert err <= 5e-6 * max(1.0, np.abs(Xm).max()), err
+    cerr = np.abs(vi.X_cov.numpy() - Xc).max()
+    assert cerr <= 1e-6 * max(1.0, np.abs(Xc).max()), cerr
+    for a, b in zip(h["elbo"], ref["elbo"]):
+        assert abs(float(a) - b) <= 5e-6 * abs(b), (float(a), b)
+    for a, b in zip(h["reconstruction_error"], ref["reconstruction_error"]):
+        assert abs(a - b) <= 5e-6 * abs(b), (a, b)
+
+
+def test_not_swap_consistent(gpu_device):
+    """Y mutated after generation (multiplicative_strength_comparison.py:161-186
+    does this): the ELBO/MSE must read both triangles."""
+    import ame_oracle as O
+    from ame_amd import TemporalAMEModel
+    m = TemporalAMEModel(30, 4, 3, seed=3)
+    m.generate_data_fast(seed=5)
+    m.Y[3, 7, 1, 0] += 0.5
+    m.Y[20, 2, 3, 1] -= 0.25
+    vi = _vi(m, "good", 0.2, gpu_device)
+    assert not vi.engine.swap_consistent
+    Xm = vi.X_mean.numpy().astype(np.float64).copy()
+    Xc = vi.X_cov.numpy().astype(np.float64).copy()
+    params = {k: getattr(m, k).numpy().astype(np.float64)
+              for k in ("R", "R_inv", "Sigma", "Psi", "Phi", "Q")}
+    ref = O.fit(m.Y.numpy().astype(np.float64), Xm, Xc, params, "good", 0.2, 1, 0.0)
+    h = vi.fit(max_iter=1, tolerance=0.0, verbose=False)
+    assert abs(h["reconstruction_error"][0] - ref["reconstruction_error"][0]) <= 5e-6 * ref["reconstruction_error"][0]
+    assert abs(float(h["elbo"][0]) - ref["elbo"][0]) <= 5e-6 * abs(ref["elbo"][0])
+
+
+def test_deterministic(gpu_device):
+    from ame_amd import TemporalAMEModel
+    outs = []
+    for _ in range(2):
+        m = TemporalAMEModel(96, 12, 4, seed=1)
+        m.generate_data_fast(seed=2)
+        vi = _vi(m, "good", 0.5, gpu_device)
+        h = vi.fit(max_iter=2, tolerance=0.0, verbose=False)
+        outs.append((vi.X_mean.numpy().copy(), vi.X_cov.numpy().copy(),
+                     [float(e) for e in h["elbo"]], list(h["reconstruction_error"])))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.array_equal(outs[0][1], outs[1][1])
+    assert outs[0][2] == outs[1][2] and outs[0][3] == outs[1][3]
