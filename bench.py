@@ -1,0 +1,227 @@
+#!/usr/bin/env python
+"""Benchmark: dyad-timestep ELBO updates/s of the temporal-AME SMF VI loop on MI355X.
+
+One "step" = one fit() iteration of TemporalAMEStructuredMFVI (reference
+base.py:170-181): Gauss-Seidel sweep + covariance update + ELBO + MSE, over the
+synthetic BASELINE config 3 workload (n=1024 nodes, latent_dim=16 -> d=34,
+T=128 time steps per GPU; weak scaling T_total = 128 * N, time-sharded).
+Units per step = T_total * n(n-1)/2 (the unordered dyad-timesteps the ELBO sums).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line.  Inputs are resident in HBM before timing; the
+timed region is K full fit() iterations bracketed by barrier + synchronize,
+max over ranks.  `roofline` is for the dominant kernel, timed with HIP events
+on the stream it runs on; `cpu_baseline` times the numpy oracle
+(oracle/ame_oracle.py) on a bounded sample of the same workload on this host.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "python-temporal-ame-svi_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "dyad-timestep ELBO updates/sec at n=1024,T=128,d=16; 1/2/4/8-GPU scaling"
+UNIT = "dyad-timestep ELBO updates/s"
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def kernel_bytes(n, TL, d, swap_consistent=True):
+    """Algorithmic HBM bytes per launch."""
+    y_full = 8.0 * n * (n - 1) * TL
+    return {
+        # Y row of every ordered dyad + old means read + new means written
+        "sweep": y_full + 8.0 * n * TL * d,
+        # old covariance read + new written + old/new means read
+        "cov": 8.0 * n * TL * d * d + 8.0 * n * TL * d,
+        # Y (upper triangle if swap-consistent) + means
+        "elbo": (y_full / 2 if swap_consistent else y_full) + 4.0 * n * TL * d,
+    }
+
+
+def cpu_baseline(model, vi, n, T, d, budget_s=20.0):
+    """Time the numpy oracle (fp32, reference dtype) on a bounded sample of the
+    same iteration and extrapolate linearly to one full iteration."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ame_oracle as O
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([p.get("num_threads", 1) for p in threadpool_info()] + [1])
+    except Exception:  # pragma: no cover
+        cores = 1
+    Y = model.Y.detach().cpu().numpy().astype(np.float32)
+    Xm = vi.X_mean.numpy().astype(np.float32).copy()
+    Xc = vi.X_cov.numpy().astype(np.float32).copy()
+    params = {k: getattr(model, k).detach().cpu().numpy().astype(np.float32)
+              for k in ("R", "R_inv", "Sigma", "Psi", "Phi", "Q")}
+    consts = O.prior_terms(params, T, np.float32)
+    # calibrate on one node
+    t0 = time.perf_counter()
+    O.update_node(Y, Xm, Xc, params, 0, "good", 0.01, consts)
+    per_node = time.perf_counter() - t0
+    k = int(max(1, min(n - 1, (0.6 * budget_s) / max(per_node, 1e-6))))
+    t0 = time.perf_counter()
+    for i in range(1, 1 + k):
+        O.update_node(Y, Xm, Xc, params, i, "good", 0.01, consts)
+    t_nodes = time.perf_counter() - t0
+    sweep_est = t_nodes / k * n
+    m = max(1, min(T, 4))
+    t0 = time.perf_counter()
+    O.expected_loglik(Y, Xm, Xc, params, "good", ts=range(m))
+    t_ll = (time.perf_counter() - t0) / m * T
+    t0 = time.perf_counter()
+    off = ~np.eye(n, dtype=bool)
+    for t in range(m):
+        mu = O.compute_mean(Xm[:, t].astype(np.float64), (d - 2) // 2)
+        float((((Y[:, :, t] - mu) ** 2)[off]).sum())
+    t_rec = (time.perf_counter() - t0) / m * T
+    kn = min(n, 32)
+    t0 = time.perf_counter()
+    O.entropy(Xc[:kn])
+    O.log_prior_transitions(Xm[:kn], Xc[:kn], params)
+    O.log_prior_initial(Xm[:kn], Xc[:kn], params)
+    t_node_terms = (time.perf_counter() - t0) / kn * n
+    it_est = sweep_est + t_ll + t_rec + t_node_terms
+    units = T * n * (n - 1) / 2.0
+    return {
+        "value": units / it_est, "unit": UNIT, "cores": int(cores), "kind": "port",
+        "sample": (f"numpy oracle fp32 on this host: update_node for {k + 1} of {n} nodes x {T} "
+                   f"slices, loglik+MSE for {m} of {T} slices, entropy/prior terms for {kn} "
+                   f"nodes; extrapolated linearly to one full iteration "
+                   f"(est. {it_est:.1f} s/iteration)"),
+    }
+
+
+def load_pmc(tag):
+    path = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        z = json.load(open(path))
+        if z.get("config_tag") != tag:
+            return None
+        return z
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=1024)
+    ap.add_argument("--t-per-gpu", type=int, default=128)
+    ap.add_argument("--latent-dim", type=int, default=16)
+    ap.add_argument("--variant", default="good", choices=["good", "bad", "naive"])
+    ap.add_argument("--lr", type=float, default=0.01)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    args = ap.parse_args()
+
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE",
+              file=sys.stderr)
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local_rank % max(ndev, 1))
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from ame_amd import TemporalAMEModel, TemporalAMENaiveMFVI, TemporalAMEStructuredMFVI
+
+    n, r = args.n, args.latent_dim
+    d = 2 + 2 * r
+    T_total = args.t_per_gpu * world
+    model = TemporalAMEModel(n, T_total, r, seed=42)
+    model.generate_data_fast(device=dev)
+    if args.variant == "naive":
+        vi = TemporalAMENaiveMFVI(model, learning_rate=args.lr, device=dev,
+                                  distributed=world > 1)
+    else:
+        vi = TemporalAMEStructuredMFVI(model, factorization=args.variant, learning_rate=args.lr,
+                                       device=dev, distributed=world > 1)
+    if args.warmup > 0:
+        vi.fit(max_iter=args.warmup, tolerance=0.0, verbose=False)
+    eng = vi.engine
+    eng.timing = True
+    eng.events.clear()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    barrier()
+    t0 = time.perf_counter()
+    hist = vi.fit(max_iter=args.steps, tolerance=0.0, verbose=False)
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    kms, kcount = eng.kernel_ms()
+    TL = eng.shard.T_local
+    kb = kernel_bytes(n, TL, d, eng.swap_consistent)
+    dom = max(kms, key=kms.get)
+    achieved = kb[dom] / (kms[dom] * 1e-3) / 1e9
+    units_per_step = T_total * n * (n - 1) / 2.0
+    value = units_per_step * args.steps / dt
+    ms_step = dt / args.steps * 1e3
+    b_iter = 8.0 * n * (n - 1) * T_total + 4.0 * n * (n - 1) * T_total \
+        + 12.0 * n * T_total * d * d + 16.0 * n * T_total * d
+    tag = f"n{n}_T{args.t_per_gpu}_r{r}_{args.variant}"
+    pmc = load_pmc(tag)
+    traffic = None
+    if pmc is not None and dom in pmc.get("kernels", {}):
+        traffic = pmc["kernels"][dom].get("hbm_bytes_per_launch")
+
+    out = None
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(model, vi, n, T_total, d, budget_s=args.cpu_budget)
+        elbo_last = float(hist["elbo"][-1])
+        out = {
+            "metric": METRIC, "value": value, "unit": UNIT, "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32", "data": "synthetic",
+            "config": {
+                "workload": (f"BASELINE config 3 shape per GPU: n_nodes={n}, n_time={args.t_per_gpu}"
+                             f"/GPU (T_total={T_total}), latent_dim={r} (d={d}), "
+                             f"SMF-{args.variant} fit iteration, lr={args.lr}"),
+                "n_nodes": n, "n_time_total": T_total, "latent_dim": r, "d": d,
+                "variant": args.variant, "parallelism": f"time-sharded x{world}",
+            },
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic},
+            "kernels_ms": kms,
+            "iteration_roofline_frac": b_iter / (dt / args.steps) / (world * HBM_PEAK_GBS * 1e9),
+            "cpu_baseline": cpu,
+            "elbo_last": elbo_last,
+            "mse_last": float(hist["reconstruction_error"][-1]),
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return out
+
+
+if __name__ == "__main__":
+    main()

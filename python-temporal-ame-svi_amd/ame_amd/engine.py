@@ -163,10 +163,34 @@ class DeviceEngine:
                 f"lanes ({self.max_slices}) for n={self.n}, r={self.r}; shard over more GPUs")
         self._out_host = None
         self._out_valid = False
+        self.timing = False       # record HIP events around each kernel launch
+        self.events = []          # (name, start, end) while timing
 
     # ------------------------------------------------------------------
     def _sp(self):
         return ctypes.c_void_p(self.stream.cuda_stream)
+
+    def _tic(self, name):
+        if not self.timing:
+            return None
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(self.stream)
+        return (name, e)
+
+    def _toc(self, tok):
+        if tok is None:
+            return
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(self.stream)
+        self.events.append((tok[0], tok[1], e))
+
+    def kernel_ms(self):
+        """Average device ms per launch of each timed kernel (synchronises)."""
+        torch.cuda.synchronize(self.dev)
+        acc = {}
+        for name, a, b in self.events:
+            acc.setdefault(name, []).append(a.elapsed_time(b))
+        return {k: sum(v) / len(v) for k, v in acc.items()}, {k: len(v) for k, v in acc.items()}
 
     def _pack_y(self, Y):
         if Y is None:
@@ -197,13 +221,17 @@ class DeviceEngine:
             hand=_ptr(self.hand), halo_in=halo_in, halo_out=halo_out, snap=_ptr(self.snap),
             consts=_ptr(self.consts), rinv=self.C.rinv4(), lr=self.lr,
             one_minus_lr=float(1.0 - self.lr), epoch=self.epoch, status=_ptr(self.status))
+        tok = self._tic("sweep")
         _lib.check(self.L.ame_sweep(ctypes.byref(self.dims), ctypes.byref(a), self._sp()),
                    "ame_sweep")
+        self._toc(tok)
         c = _lib.ame_cov_args(
             x_old=_ptr(self.x_a), x_new=_ptr(self.x_b), cov=_ptr(self.cov), snap=_ptr(self.snap),
             consts=_ptr(self.consts), cov_terms=_ptr(self.cov_terms), rinv=self.C.rinv4(),
             lr=self.lr, one_minus_lr=float(1.0 - self.lr), update=1)
+        tok = self._tic("cov")
         _lib.check(self.L.ame_cov(ctypes.byref(self.dims), ctypes.byref(c), self._sp()), "ame_cov")
+        self._toc(tok)
         self.x_a, self.x_b = self.x_b, self.x_a
         self._out_valid = False
         self._cov_terms_valid = True
@@ -230,8 +258,10 @@ class DeviceEngine:
             cov_terms=_ptr(self.cov_terms), consts=_ptr(self.consts), phi=_ptr(self.phi),
             rinv=self.C.rinv4(), swap_consistent=1 if self.swap_consistent else 0,
             work=_ptr(self.work), out=_ptr(self.out))
+        tok = self._tic("elbo")
         _lib.check(self.L.ame_elbo(ctypes.byref(self.dims), ctypes.byref(e), self._sp()),
                    "ame_elbo")
+        self._toc(tok)
 
     def sums(self):
         """The 8 fp64 sums for the current state (all ranks reduced)."""
