@@ -146,6 +146,12 @@ int ame_elbo(const ame_dims* dims, const ame_elbo_args* args, void* stream);
 /* Scratch doubles ame_elbo needs. */
 long long ame_elbo_work_size(const ame_dims* dims);
 
+/* Pin + map host memory (e.g. a shared-memory halo buffer mapped by two
+ * processes) for device access; *dev receives the device address.  Used by the
+ * time-sharded multi-GPU path for the boundary-mean granule hand-off. */
+int ame_host_register(void* host, unsigned long long bytes, void** dev);
+int ame_host_unregister(void* host);
+
 /* Latent dims compiled into this library (fills up to cap entries, returns count). */
 int ame_supported_r(int* out, int cap);
 

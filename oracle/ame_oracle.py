@@ -156,6 +156,38 @@ def update_node(Y, X_mean, X_cov, params, i, variant, lr, consts=None):
         X_cov[i, t] = dt.type(lr) * C + dt.type(1 - lr) * X_cov[i, t]
 
 
+def update_step(Y, X_mean, X_cov, params, i, t, variant, lr, consts, T_total=None, t_off=0):
+    """One (node i, local slice t) step of update_node, for time-sharded replays:
+    X_mean holds local slices plus halo slots; global time = t + t_off."""
+    n, TL, d = X_mean.shape
+    T = TL if T_total is None else T_total
+    tg = t + t_off
+    dt = X_mean.dtype
+    Q_inv, S0_inv, PtQiP = consts
+    Phi = params["Phi"]
+    P, h = observation_terms(Y, X_mean, params["R_inv"], i, t)
+    if tg == 0:
+        P = P + S0_inv
+    if tg > 0:
+        P = P + Q_inv
+        h = h + Q_inv @ (Phi @ X_mean[i, t - 1])
+    if tg < T - 1:
+        P = P + PtQiP
+        h = h + Phi.T @ (Q_inv @ X_mean[i, t + 1])
+    if variant == "naive":
+        mu = np.linalg.solve(P, h)
+        C = np.diag(dt.type(1.0) / (np.diag(P) + dt.type(1e-8))).astype(dt)
+    else:
+        C = _inv(P)
+        if variant == "bad":
+            C[:2, 2:] = 0
+            C[2:, :2] = 0
+        C = (C + C.T) / dt.type(2) + np.eye(d, dtype=dt) * dt.type(1e-6)
+        mu = C @ h
+    X_mean[i, t] = dt.type(lr) * mu + dt.type(1 - lr) * X_mean[i, t]
+    X_cov[i, t] = dt.type(lr) * C + dt.type(1 - lr) * X_cov[i, t]
+
+
 def sweep(Y, X_mean, X_cov, params, variant, lr, nodes=None):
     """_update_step: sequential Gauss-Seidel over nodes (structured_mf.py:217-218)."""
     n, T, d = X_mean.shape

@@ -10,7 +10,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libame_amd.so")
+LIB_PATH = os.environ.get("AME_LIB_PATH") or os.path.join(_HERE, "libame_amd.so")
 
 AME_GOOD, AME_BAD, AME_NAIVE = 0, 1, 2
 AME_STATUS_SPIN_TIMEOUT = 1
@@ -46,7 +46,8 @@ class ame_elbo_args(ctypes.Structure):
 
 # every symbol include/ame_amd.h declares (checked by tests/test_capi.py)
 EXPORTS = ("ame_pack_y", "ame_sweep", "ame_sweep_max_slices", "ame_sweep_lds_bytes", "ame_cov",
-           "ame_elbo", "ame_elbo_work_size", "ame_supported_r", "ame_last_error", "ame_version")
+           "ame_elbo", "ame_elbo_work_size", "ame_host_register", "ame_host_unregister",
+           "ame_supported_r", "ame_last_error", "ame_version")
 
 _lock = threading.Lock()
 _lib = None
@@ -64,10 +65,12 @@ def _declare(L):
     L.ame_elbo_work_size.argtypes = [P(ame_dims)]
     L.ame_elbo_work_size.restype = ctypes.c_longlong
     L.ame_supported_r.argtypes = [P(ctypes.c_int), ctypes.c_int]
+    L.ame_host_register.argtypes = [c_vp, ctypes.c_ulonglong, P(c_vp)]
+    L.ame_host_unregister.argtypes = [c_vp]
     L.ame_last_error.restype = ctypes.c_char_p
     L.ame_version.restype = ctypes.c_char_p
     for name in ("ame_pack_y", "ame_sweep", "ame_cov", "ame_elbo", "ame_sweep_max_slices",
-                 "ame_supported_r"):
+                 "ame_supported_r", "ame_host_register", "ame_host_unregister"):
         getattr(L, name).restype = ctypes.c_int
     return L
 

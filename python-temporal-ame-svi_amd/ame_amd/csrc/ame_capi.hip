@@ -65,6 +65,27 @@ int ame_supported_r(int* out, int cap) {
     return c;
 }
 
+int ame_host_register(void* host, unsigned long long bytes, void** dev) {
+    if (!host || !dev || bytes == 0) return fail("ame_host_register: bad arguments");
+    hipError_t e = hipHostRegister(host, (size_t)bytes, hipHostRegisterMapped | hipHostRegisterPortable);
+    if (e != hipSuccess) {
+        snprintf(g_err, sizeof(g_err), "ame_host_register: hipHostRegister: %s", hipGetErrorString(e));
+        return -1;
+    }
+    e = hipHostGetDevicePointer(dev, host, 0);
+    if (e != hipSuccess) {
+        snprintf(g_err, sizeof(g_err), "ame_host_register: hipHostGetDevicePointer: %s",
+                 hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+}
+
+int ame_host_unregister(void* host) {
+    if (!host) return fail("ame_host_unregister: NULL");
+    return hipHostUnregister(host) == hipSuccess ? 0 : fail("ame_host_unregister failed");
+}
+
 long long ame_sweep_lds_bytes(int n, int r) {
     if (!r_supported(r) || n < 1) return 0;
     return sweep_lds_layout(n, r).total;

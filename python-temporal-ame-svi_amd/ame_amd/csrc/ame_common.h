@@ -14,7 +14,10 @@
 
 #define AME_NT 256          // threads per workgroup
 #define AME_SNAP_NB 16      // sweep statistic snapshot stride (nodes)
-#define AME_SPIN_LIMIT (1u << 21)
+// Spin bounds in s_memrealtime ticks (constant 100 MHz clock): a hand-off that
+// does not arrive within this time sets a status bit and the sweep finishes.
+#define AME_SPIN_TICKS_LOCAL (200ull * 1000 * 1000)   // 2 s, lane -> lane on one GPU
+#define AME_SPIN_TICKS_HALO (1000ull * 1000 * 1000)   // 10 s, rank -> rank
 
 template <int R>
 struct AmeCfg {
@@ -178,4 +181,8 @@ __host__ __device__ inline SweepLds sweep_lds_layout(int n, int R) {
     return L;
 }
 
+#ifdef AME_ONLY_R   // diagnostic builds: one latent dim only
+#define AME_FOR_EACH_R(X) X(AME_ONLY_R)
+#else
 #define AME_FOR_EACH_R(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(12) X(16) X(24)
+#endif

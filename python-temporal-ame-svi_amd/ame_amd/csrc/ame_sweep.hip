@@ -22,6 +22,33 @@
 //     covariance kernel can rebuild bit-identical precisions in parallel.
 #include "ame_common.h"
 
+#ifdef AME_STAMPS
+// Diagnostic build only (cdna_hip_programming.md §7, in-kernel stamps): lane
+// AME_STAMP_LANE records s_memtime after each phase for nodes
+// [AME_STAMP_I0, AME_STAMP_I0 + 16).  Never compiled into the product library.
+#define AME_STAMP_I0 256
+#define AME_STAMP_NPH 8
+__device__ unsigned long long g_ame_stamps[16 * AME_STAMP_NPH];
+#define STAMP(ph)                                                                          \
+    do {                                                                                   \
+        if (stamp_on && tid == 0) {                                                        \
+            unsigned long long t_;                                                         \
+            __builtin_amdgcn_sched_barrier(0);                                             \
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");     \
+            __builtin_amdgcn_sched_barrier(0);                                             \
+            g_ame_stamps[(i - AME_STAMP_I0) * AME_STAMP_NPH + (ph)] = t_;                  \
+        }                                                                                  \
+    } while (0)
+extern "C" int ame_debug_read_stamps(unsigned long long* host, int count) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ame_stamps), sizeof(unsigned long long) * count,
+                               0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#else
+#define STAMP(ph) \
+    do {          \
+    } while (0)
+#endif
+
 template <int R>
 __global__ void __launch_bounds__(AME_NT)
 ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
@@ -106,6 +133,10 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     float* xn = a.x_new + (size_t)tl * n * D;
 
     for (int i = 0; i < n; ++i) {
+#ifdef AME_STAMPS
+        const bool stamp_on = (tl == TL / 2) && i >= AME_STAMP_I0 && i < AME_STAMP_I0 + 16;
+#endif
+        STAMP(0);
         // (a) statistic snapshot for the covariance kernel
         if ((i % AME_SNAP_NB) == 0) {
             double* dst = a.snap + ((size_t)tl * nblk + i / AME_SNAP_NB) * NS;
@@ -138,7 +169,8 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 const uint64_t* src = from_halo ? a.halo_in + (size_t)i * D
                                                 : a.hand + ((size_t)(tl - 1) * n + i) * D;
                 uint64_t v = 0;
-                unsigned spins = 0;
+                const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+                const uint64_t budget = from_halo ? AME_SPIN_TICKS_HALO : AME_SPIN_TICKS_LOCAL;
                 while (true) {
                     bool ok = true;
                     if (k < D) {
@@ -146,14 +178,14 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                         ok = (uint32_t)(v >> 32) == a.epoch;
                     }
                     if (__all(ok) || dead) break;
-                    if (++spins > AME_SPIN_LIMIT) {
+                    if (__builtin_amdgcn_s_memrealtime() - t_start > budget) {
                         if (k == 0)
                             atomicOr(a.status, from_halo ? AME_STATUS_HALO_TIMEOUT
                                                          : AME_STATUS_SPIN_TIMEOUT);
                         dead = true;
                         break;
                     }
-                    __builtin_amdgcn_s_sleep(1);
+                    __builtin_amdgcn_s_sleep(2);
                 }
                 if (k < D) mu_prev[k] = __uint_as_float((uint32_t)v);
             }
@@ -161,6 +193,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             mu_prev[tid] = 0.f;
         }
         __syncthreads();   // B1
+        STAMP(1);
 
         // (d) GEMV partials: h_U = sum_j z0_j V_j, h_V = sum_j z1_j U_j (+ sums of z)
         {
@@ -218,6 +251,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             }
         }
         __syncthreads();   // B2
+        STAMP(2);
 
         // (e) natural parameter (reduce partials) and augmented precision [P | rhs]
         if (tid < PW) {
@@ -246,6 +280,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             }
         }
         __syncthreads();   // B3
+        STAMP(3);
 
         // (f) Gauss-Jordan elimination (SPD: no pivoting), fp64
         for (int pv = 0; pv < D; ++pv) {
@@ -261,6 +296,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             __syncthreads();
         }
 
+        STAMP(4);
         // (g) new mean: mu* = C h with C = sym(P^-1) (+1e-6 I), damped
         if (tid < D) {
             const int k = tid;
@@ -277,6 +313,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 gran_store_system(a.halo_out + (size_t)i * D + k, gv);
         }
         __syncthreads();   // B4
+        STAMP(5);
 
         // (h) statistics: S += stat(new) - stat(old)
         {
@@ -285,6 +322,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 S[e] = stat_apply<R>(S[e], e, mu_new + 2, mu_new + 2 + R, Uo, Uo + R);
         }
         __syncthreads();   // B5
+        STAMP(6);
         if (tid < M2) M[i * M2 + tid] = mu_new[2 + tid];
     }
 }

@@ -1,0 +1,80 @@
+"""The C-ABI library loads and exports every symbol include/ame_amd.h declares.
+
+No compute calls here (no GPU in the build container): only the host-side
+entry points that never touch the device, and argument validation, which
+returns before any HIP call.
+"""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+
+def _lib():
+    from ame_amd import _lib as L
+    if not os.path.exists(L.LIB_PATH):
+        from ame_amd.build import build
+        build(verbose=False)
+    return L
+
+
+def _header_symbols():
+    txt = open(os.path.join(ROOT, "include", "ame_amd.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(ame_[a-z_0-9]+)\s*\(", txt)))
+
+
+def test_header_symbols_exported():
+    L = _lib()
+    lib = L.lib()
+    syms = _header_symbols()
+    assert len(syms) >= 10
+    for s in syms:
+        assert hasattr(lib, s), f"{s} declared in include/ame_amd.h but not exported"
+    assert set(syms) == set(L.EXPORTS)
+
+
+def test_host_only_entry_points():
+    L = _lib()
+    lib = L.lib()
+    assert b"gfx950" in lib.ame_version()
+    rs = L.supported_r()
+    for r in (1, 2, 3, 8, 16):
+        assert r in rs
+    # LDS budget of the sweep's per-slice state: config 3 (n=1024, r=16) fits one CU
+    assert 0 < lib.ame_sweep_lds_bytes(1024, 16) <= 160 * 1024
+    assert lib.ame_sweep_lds_bytes(1024, 999) == 0
+    d = L.ame_dims(1024, 16, 128, 0, 128, L.AME_GOOD)
+    assert lib.ame_elbo_work_size(ctypes.byref(d)) > 0
+
+
+def test_argument_validation_fails_loudly():
+    L = _lib()
+    lib = L.lib()
+    d = L.ame_dims(16, 2, 4, 0, 4, L.AME_GOOD)
+    a = L.ame_sweep_args()
+    rc = lib.ame_sweep(ctypes.byref(d), ctypes.byref(a), None)
+    assert rc != 0 and b"NULL" in lib.ame_last_error()
+    bad = L.ame_dims(16, 999, 4, 0, 4, L.AME_GOOD)
+    assert lib.ame_sweep(ctypes.byref(bad), ctypes.byref(a), None) != 0
+    assert b"latent_dim" in lib.ame_last_error()
+    rng = L.ame_dims(16, 2, 4, 2, 4, L.AME_GOOD)   # slices [2, 6) outside T=4
+    assert lib.ame_cov(ctypes.byref(rng), ctypes.byref(L.ame_cov_args()), None) != 0
+    with pytest.raises(RuntimeError):
+        L.check(-1, "ame_sweep")
+
+
+def test_no_cpu_fallback():
+    """The product path refuses to run without a GPU instead of falling back."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from ame_amd import TemporalAMEModel, TemporalAMEStructuredMFVI
+    m = TemporalAMEModel(6, 3, 2, seed=1)
+    m.generate_data()
+    vi = TemporalAMEStructuredMFVI(m)
+    with pytest.raises(RuntimeError, match="no GPU"):
+        vi.fit(max_iter=1, verbose=False)

@@ -1,0 +1,76 @@
+"""Time-sharded sweep on the GPU: 2 ranks (processes) on one MI355X, boundary
+means handed over through the host-mapped granule buffer while both sweep
+kernels run.  Must reproduce the single-process result bit for bit (means,
+covariances) and the ELBO/MSE to fp64 round-off."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(n, T, r, method, lr, iters, distributed):
+    from ame_amd import TemporalAMEModel, TemporalAMENaiveMFVI, TemporalAMEStructuredMFVI
+    m = TemporalAMEModel(n, T, r, seed=21)
+    m.generate_data_fast(seed=4)
+    dev = torch.device("cuda", 0)
+    if method == "naive":
+        vi = TemporalAMENaiveMFVI(m, learning_rate=lr, device=dev, distributed=distributed)
+    else:
+        vi = TemporalAMEStructuredMFVI(m, factorization=method, learning_rate=lr, device=dev,
+                                       distributed=distributed)
+    h = vi.fit(max_iter=iters, tolerance=0.0, verbose=False)
+    return (vi.X_mean.numpy().copy(), vi.X_cov.numpy().copy(),
+            [float(e) for e in h["elbo"]], list(h["reconstruction_error"]))
+
+
+def _worker(rank, world, port, args, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = _run(*args, distributed=True)
+        if rank == 0:
+            q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n,T,r,method,lr", [(64, 8, 4, "good", 0.5), (40, 6, 3, "bad", 1.0),
+                                             (48, 5, 2, "naive", 0.3)])
+def test_two_ranks_one_gpu(n, T, r, method, lr):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    args = (n, T, r, method, lr, 3)
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(rk, 2, port, args, q)) for rk in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=150)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.exitcode is None:
+            p.kill()
+            p.join()
+    assert codes == [0, 0], f"rank exit codes {codes}"
+    mean_d, cov_d, elbo_d, rec_d = q.get()
+    mean_s, cov_s, elbo_s, rec_s = _run(*args, distributed=False)
+    assert np.array_equal(mean_d, mean_s)
+    assert np.array_equal(cov_d, cov_s)
+    assert np.allclose(elbo_d, elbo_s, rtol=1e-6, atol=0)
+    assert np.allclose(rec_d, rec_s, rtol=1e-12, atol=0)
