@@ -107,21 +107,25 @@ def _worker(rank, world, port, n, T, r, method, lr, q):
 def test_time_sharded_sweep_matches_unsharded(n, T, r, method, lr):
     world = 2
     ctx = mp.get_context("spawn")
-    q = ctx.SimpleQueue()
+    q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(rk, world, port, n, T, r, method, lr, q))
              for rk in range(world)]
     for p in procs:
         p.start()
+    try:
+        result = q.get(timeout=240)   # read before join: a large put blocks the child
+    except Exception:
+        result = None
     for p in procs:
-        p.join(timeout=240)
+        p.join(timeout=30)
     codes = [p.exitcode for p in procs]
     for p in procs:
         if p.exitcode is None:
             p.kill()
             p.join()
     assert codes == [0, 0], f"rank exit codes {codes}"
-    mean_s, cov_s, terms = q.get()
+    mean_s, cov_s, terms = result
     Y, Xm, Xc, P, m = _setup(n, T, r, seed=11)
     for _ in range(2):
         O.sweep(Y, Xm, Xc, P, method, lr)

@@ -55,20 +55,24 @@ def test_two_ranks_one_gpu(n, T, r, method, lr):
         pytest.skip("no GPU")
     args = (n, T, r, method, lr, 3)
     ctx = mp.get_context("spawn")
-    q = ctx.SimpleQueue()
+    q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(rk, 2, port, args, q)) for rk in range(2)]
     for p in procs:
         p.start()
+    try:
+        result = q.get(timeout=150)   # read before join: a large put blocks the child
+    except Exception:
+        result = None
     for p in procs:
-        p.join(timeout=150)
+        p.join(timeout=30)
     codes = [p.exitcode for p in procs]
     for p in procs:
         if p.exitcode is None:
             p.kill()
             p.join()
     assert codes == [0, 0], f"rank exit codes {codes}"
-    mean_d, cov_d, elbo_d, rec_d = q.get()
+    mean_d, cov_d, elbo_d, rec_d = result
     mean_s, cov_s, elbo_s, rec_s = _run(*args, distributed=False)
     assert np.array_equal(mean_d, mean_s)
     assert np.array_equal(cov_d, cov_s)
