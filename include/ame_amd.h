@@ -15,12 +15,10 @@
  *   ame_sweep         replaces _update_step -> _update_node_i ->
  *                     _compute_observation_terms (structured_mf.py:211-326,
  *                     naive_mf.py:193-376): the sequential Gauss-Seidel sweep,
- *                     means only.
- *   ame_cov           replaces the covariance half of _update_node_i
- *                     (structured_mf.py:266-287; naive_mf.py:270-282) and
- *                     produces the per-(node,time) covariance terms of the ELBO
+ *                     new means AND new (damped) covariances.
+ *   ame_cov           the per-(node,time) covariance terms of the ELBO
  *                     (_compute_entropy :202-209, trace terms :142-144, :166,
- *                     :193).
+ *                     :193) of the stored covariances.
  *   ame_elbo          replaces _compute_elbo (structured_mf.py:115-209,
  *                     naive_mf.py:89-191) and
  *                     compute_temporal_reconstruction_error
@@ -74,7 +72,7 @@ typedef struct ame_sweep_args {
     const uint64_t* halo_in;     /* [n][d] granules of slice t_begin-1 (left rank), or NULL */
     uint64_t* halo_out;          /* [n][d] granules of slice t_begin+T_local-1 for the right
                                     rank (peer/host-mapped), or NULL */
-    double* snap;                /* [T_local][ceil(n/16)][2r+3r^2] fp64 statistic snapshots */
+    float* cov;                  /* [T_local][n][d][d] covariances, damped in place */
     const double* consts;        /* fp64 [5][d][d] */
     double rinv[4];              /* R_inv row-major (host values) */
     float lr;                    /* learning_rate (damping) */
@@ -84,16 +82,9 @@ typedef struct ame_sweep_args {
 } ame_sweep_args;
 
 typedef struct ame_cov_args {
-    const float* x_old;          /* [T_local][n][d] */
-    const float* x_new;          /* [T_local][n][d] */
-    float* cov;                  /* [T_local][n][d][d] updated in place */
-    const double* snap;          /* as written by ame_sweep */
+    const float* cov;            /* [T_local][n][d][d] */
     const double* consts;        /* fp64 [5][d][d] */
     double* cov_terms;           /* [T_local][n][4] fp64: logdet, trace, tr(Qinv S), tr(S0inv S) */
-    double rinv[4];
-    float lr;
-    float one_minus_lr;
-    int32_t update;              /* 1: damped update from the sweep; 0: terms of cov as-is */
 } ame_cov_args;
 
 typedef struct ame_elbo_args {
@@ -115,11 +106,11 @@ typedef struct ame_elbo_args {
 int ame_pack_y(const float* Y, float* Yt, const ame_dims* dims,
                unsigned long long* mismatch, void* stream);
 
-/* One Gauss-Seidel sweep over all n nodes for the local slices (means only).
- * One workgroup per local slice; all T_local workgroups must be co-resident
- * (see ame_sweep_max_slices).  Reproduces the reference node order exactly:
- * step (i,t) sees new means of nodes j<i at t and of node i at t-1, and old
- * means of nodes j>i at t and of node i at t+1. */
+/* One Gauss-Seidel sweep over all n nodes for the local slices: new means and
+ * new (damped) covariances.  One workgroup per local slice; all T_local
+ * workgroups must be co-resident (see ame_sweep_max_slices).  Reproduces the
+ * reference node order exactly: step (i,t) sees new means of nodes j<i at t
+ * and of node i at t-1, and old means of nodes j>i at t and of node i at t+1. */
 int ame_sweep(const ame_dims* dims, const ame_sweep_args* args, void* stream);
 
 /* Largest T_local ame_sweep can run with for (n, r) on this device, 0 if the
@@ -129,10 +120,8 @@ int ame_sweep_max_slices(int n, int r);
 /* Dynamic LDS bytes ame_sweep needs per workgroup (0 = unsupported r). */
 long long ame_sweep_lds_bytes(int n, int r);
 
-/* Covariance update for every (node, local slice) in parallel, reconstructing
- * each step's precision from the sweep's statistic snapshots (bit-identical to
- * the precision the sweep solved with), plus the per-(node,time) covariance
- * terms of the ELBO. */
+/* Per-(node, local slice) covariance terms of the ELBO (log|S|, tr S,
+ * tr(Qinv S), tr(S0inv S)), fully parallel: one wave per covariance. */
 int ame_cov(const ame_dims* dims, const ame_cov_args* args, void* stream);
 
 /* ELBO / reconstruction sufficient sums over the local slices:

@@ -27,15 +27,13 @@ class ame_dims(ctypes.Structure):
 
 class ame_sweep_args(ctypes.Structure):
     _fields_ = [("Yt", c_vp), ("x_old", c_vp), ("x_new", c_vp), ("next_old", c_vp),
-                ("hand", c_vp), ("halo_in", c_vp), ("halo_out", c_vp), ("snap", c_vp),
+                ("hand", c_vp), ("halo_in", c_vp), ("halo_out", c_vp), ("cov", c_vp),
                 ("consts", c_vp), ("rinv", ctypes.c_double * 4), ("lr", ctypes.c_float),
                 ("one_minus_lr", ctypes.c_float), ("epoch", ctypes.c_uint32), ("status", c_vp)]
 
 
 class ame_cov_args(ctypes.Structure):
-    _fields_ = [("x_old", c_vp), ("x_new", c_vp), ("cov", c_vp), ("snap", c_vp),
-                ("consts", c_vp), ("cov_terms", c_vp), ("rinv", ctypes.c_double * 4),
-                ("lr", ctypes.c_float), ("one_minus_lr", ctypes.c_float), ("update", c_int32)]
+    _fields_ = [("cov", c_vp), ("consts", c_vp), ("cov_terms", c_vp)]
 
 
 class ame_elbo_args(ctypes.Structure):

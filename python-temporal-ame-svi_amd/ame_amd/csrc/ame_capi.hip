@@ -111,7 +111,7 @@ int ame_pack_y(const float* Y, float* Yt, const ame_dims* dims, unsigned long lo
 
 int ame_sweep(const ame_dims* dims, const ame_sweep_args* a, void* stream) {
     if (int e = check_dims(dims)) return e;
-    if (!a || !a->Yt || !a->x_old || !a->x_new || !a->hand || !a->snap || !a->consts || !a->status)
+    if (!a || !a->Yt || !a->x_old || !a->x_new || !a->cov || !a->hand || !a->consts || !a->status)
         return fail("ame_sweep: NULL buffer");
     if (a->epoch == 0) return fail("ame_sweep: epoch must be >= 1");
     if (dims->t_begin > 0 && !a->halo_in)
@@ -129,9 +129,7 @@ int ame_sweep(const ame_dims* dims, const ame_sweep_args* a, void* stream) {
 
 int ame_cov(const ame_dims* dims, const ame_cov_args* a, void* stream) {
     if (int e = check_dims(dims)) return e;
-    if (!a || !a->x_old || !a->x_new || !a->cov || !a->consts || !a->cov_terms)
-        return fail("ame_cov: NULL buffer");
-    if (a->update && !a->snap) return fail("ame_cov: update needs snap");
+    if (!a || !a->cov || !a->consts || !a->cov_terms) return fail("ame_cov: NULL buffer");
     return launched(ame_cov_dispatch(dims, a, (hipStream_t)stream), "cov");
 }
 

@@ -1,11 +1,4 @@
 // Shared device helpers for the temporal-AME VI kernels (gfx950 / CDNA4).
-//
-// The sweep kernel (ame_sweep.hip) and the covariance kernel (ame_cov.hip) must
-// build BIT-IDENTICAL precision matrices for step (i,t): the covariance kernel
-// replays the sweep's running statistics from snapshots.  Every operation on
-// that path therefore goes through the explicitly-rounded helpers below
-// (__dadd_rn / __dsub_rn / __dmul_rn), so no FMA contraction can make the two
-// kernels diverge.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -13,97 +6,10 @@
 #include "../../../include/ame_amd.h"
 
 #define AME_NT 256          // threads per workgroup
-#define AME_SNAP_NB 16      // sweep statistic snapshot stride (nodes)
 // Spin bounds in s_memrealtime ticks (constant 100 MHz clock): a hand-off that
 // does not arrive within this time sets a status bit and the sweep finishes.
 #define AME_SPIN_TICKS_LOCAL (200ull * 1000 * 1000)   // 2 s, lane -> lane on one GPU
 #define AME_SPIN_TICKS_HALO (1000ull * 1000 * 1000)   // 10 s, rank -> rank
-
-template <int R>
-struct AmeCfg {
-    static constexpr int D = 2 + 2 * R;            // state dim
-    static constexpr int M2 = 2 * R;               // (U, V) width
-    static constexpr int NS = 2 * R + 3 * R * R;   // running statistics
-    // GEMV vector width: a chunk never straddles the U/V halves.
-    static constexpr int VEC = (R % 4 == 0) ? 4 : ((R % 2 == 0) ? 2 : 1);
-    static constexpr int CW = M2 / VEC;            // column chunks
-    static constexpr int G = AME_NT / CW;          // node groups
-    static constexpr int PW = M2 + 2;              // partial row width (+ sum z0, sum z1)
-    static constexpr int W = D + 2;                // augmented matrix row stride
-    static constexpr int QN = (D * D + AME_NT - 1) / AME_NT;   // P entries per thread
-    static constexpr int MC = (D + 3) / 4;         // AR matvec columns per thread
-};
-
-// ---------------------------------------------------------------------------
-// Running statistics of node means at one time slice.  Entry e:
-//   [0,R)            sum U_k
-//   [R,2R)           sum V_k
-//   [2R,2R+R^2)      sum U_k U_l     (k*R + l)
-//   [.., +R^2)       sum V_k V_l
-//   [.., +R^2)       sum V_k U_l
-// These are the sufficient statistics of P_obs: the reference
-// accumulates J^T R^-1 J over j != i (structured_mf.py:303-324).
-// ---------------------------------------------------------------------------
-template <int R>
-__device__ __forceinline__ double stat_val(int e, const float* U, const float* V) {
-    constexpr int R2 = R * R;
-    if (e < R) return (double)U[e];
-    if (e < 2 * R) return (double)V[e - R];
-    int f = e - 2 * R;
-    if (f < R2) { int k = f / R, l = f - k * R; return __dmul_rn((double)U[k], (double)U[l]); }
-    f -= R2;
-    if (f < R2) { int k = f / R, l = f - k * R; return __dmul_rn((double)V[k], (double)V[l]); }
-    f -= R2;
-    { int k = f / R, l = f - k * R; return __dmul_rn((double)V[k], (double)U[l]); }
-}
-
-// S[e] += stat(new) - stat(old): the only way the statistics ever change.
-template <int R>
-__device__ __forceinline__ double stat_apply(double s, int e, const float* Un, const float* Vn,
-                                             const float* Uo, const float* Vo) {
-    return __dadd_rn(s, __dsub_rn(stat_val<R>(e, Un, Vn), stat_val<R>(e, Uo, Vo)));
-}
-
-// P_obs[k][m] for node i from S (all nodes, current) minus node i's own (old)
-// contribution.  J_j = [[1,0,V_j,0],[0,1,0,U_j]] (structured_mf.py:309-320);
-// q = symmetrised off-diagonal of R_inv.
-template <int R>
-__device__ __forceinline__ double pobs_entry(int k, int m, const double* S, const float* Uo,
-                                             const float* Vo, double p, double q, double s,
-                                             double nm1) {
-    constexpr int R2 = R * R;
-    if (k < 2 && m < 2) {
-        const double c = (k == 0 && m == 0) ? p : ((k == 1 && m == 1) ? s : q);
-        return __dmul_rn(c, nm1);
-    }
-    if (k < 2 || m < 2) {
-        const int ab = (k < 2) ? k : m;
-        const int c = ((k < 2) ? m : k) - 2;
-        if (c < R) {   // U_c column: a -> p*sum V_c, b -> q*sum V_c
-            const double sv = __dsub_rn(S[R + c], (double)Vo[c]);
-            return __dmul_rn(ab == 0 ? p : q, sv);
-        }
-        const double su = __dsub_rn(S[c - R], (double)Uo[c - R]);   // V column
-        return __dmul_rn(ab == 0 ? q : s, su);
-    }
-    const int ck = k - 2, cm = m - 2;
-    if (ck < R && cm < R) {   // U,U block: p * sum V_ck V_cm
-        const int e = 2 * R + R2 + ck * R + cm;
-        return __dmul_rn(p, __dsub_rn(S[e], __dmul_rn((double)Vo[ck], (double)Vo[cm])));
-    }
-    if (ck >= R && cm >= R) {   // V,V block: s * sum U U
-        const int e = 2 * R + (ck - R) * R + (cm - R);
-        return __dmul_rn(s, __dsub_rn(S[e], __dmul_rn((double)Uo[ck - R], (double)Uo[cm - R])));
-    }
-    if (ck < R) {   // row U_ck, col V_(cm-R): q * sum V_ck U_(cm-R)
-        const int e = 2 * R + 2 * R2 + ck * R + (cm - R);
-        return __dmul_rn(q, __dsub_rn(S[e], __dmul_rn((double)Vo[ck], (double)Uo[cm - R])));
-    }
-    {   // row V_(ck-R), col U_cm: q * sum V_cm U_(ck-R)
-        const int e = 2 * R + 2 * R2 + cm * R + (ck - R);
-        return __dmul_rn(q, __dsub_rn(S[e], __dmul_rn((double)Vo[cm], (double)Uo[ck - R])));
-    }
-}
 
 // Constant part of the precision at global time tg (structured_mf.py:251-264):
 //   [t==0] Sigma0^-1 + [t>0] Q^-1 + [t<T-1] Phi^T Q^-1 Phi.
@@ -160,21 +66,24 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* scratch /* 4*
 
 // Dynamic LDS carve-up of the sweep kernel (host and device agree).
 struct SweepLds {
-    long long oS, oA, oVh, oVar, oF, oPart, oZ, oM, total;
+    long long oK, oVec, oUpd, oRed, oScal, oG, oSsq, oF, oPart, oZ, oM, total;
 };
 __host__ __device__ inline long long ame_align16(long long x) { return (x + 15) & ~15LL; }
 __host__ __device__ inline SweepLds sweep_lds_layout(int n, int R) {
-    const int D = 2 + 2 * R, M2 = 2 * R, NS = 2 * R + 3 * R * R, W = D + 2;
+    const int D = 2 + 2 * R, M2 = 2 * R, KS = D + 1, US = (M2 + 15) / 16;
     const int VEC = (R % 4 == 0) ? 4 : ((R % 2 == 0) ? 2 : 1);
-    const int G = AME_NT / (M2 / VEC);
+    const int GW = 192 / (M2 / VEC);
     SweepLds L;
     long long o = 0;
-    L.oS = o;    o = ame_align16(o + 8LL * NS);
-    L.oA = o;    o = ame_align16(o + 8LL * D * W);
-    L.oVh = o;   o = ame_align16(o + 8LL * D);
-    L.oVar = o;  o = ame_align16(o + 8LL * D);
-    L.oF = o;    o = ame_align16(o + 4LL * 4 * D);          // mu_prev, mu_next, mu_old, mu_new
-    L.oPart = o; o = ame_align16(o + 4LL * G * (M2 + 2));
+    L.oK = o;    o = ame_align16(o + 8LL * D * KS);
+    L.oVec = o;  o = ame_align16(o + 8LL * (5 + US) * D);
+    L.oUpd = o;  o = ame_align16(o + 8LL * 8 * D);
+    L.oRed = o;  o = ame_align16(o + 8LL * 16 * D);
+    L.oScal = o; o = ame_align16(o + 8LL * 64);
+    L.oG = o;    o = ame_align16(o + 8LL * 2 * D);
+    L.oSsq = o;  o = ame_align16(o + 8LL * (2 * R + D));
+    L.oF = o;    o = ame_align16(o + 4LL * 5 * D);
+    L.oPart = o; o = ame_align16(o + 4LL * GW * (M2 + 2));
     L.oZ = o;    o = ame_align16(o + 8LL * n);
     L.oM = o;    o = ame_align16(o + 4LL * n * M2);
     L.total = o;

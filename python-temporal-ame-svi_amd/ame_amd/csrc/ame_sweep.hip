@@ -1,37 +1,49 @@
-// K1: the Gauss-Seidel sweep (means only) of TemporalAMEStructuredMFVI /
-// TemporalAMENaiveMFVI for gfx950.
+// K1: the Gauss-Seidel sweep of TemporalAMEStructuredMFVI / TemporalAMENaiveMFVI
+// on gfx950: new means AND new covariances of every (node, time) step.
 //
 // Reference semantics (Alfieriek/Python-Temporal-AME-SVI):
-//   _update_step            structured_mf.py:211-218  (for i in range(n))
-//   _update_node_i          structured_mf.py:220-287  (for t in range(T))
+//   _update_step                structured_mf.py:211-218  (for i in range(n))
+//   _update_node_i              structured_mf.py:220-287  (for t in range(T))
 //   _compute_observation_terms  structured_mf.py:289-326
-//   naive variant           naive_mf.py:207-282 (mu = solve(P, h))
+//   naive variant               naive_mf.py:207-282 (mu = solve(P,h), C = diag(1/diag P))
 // Step (i,t) reads the NEW means of nodes j<i at t and of node i at t-1 and the
-// OLD means of nodes j>i at t and of node i at t+1, so one sweep is a 2-D
-// wavefront.  Design:
-//   * one workgroup per time slice ("lane" t), all lanes co-resident;
-//   * the lane keeps its slice's (U,V) means in LDS and fp64 running
-//     statistics S_t = sum_j stat(U_j, V_j) (SURVEY App. A closed form), so
-//     P_obs(i,t) = F(S_t - stat(node i)) costs O(r^2) instead of O(n r^2);
-//   * h_obs(i,t) is a GEMV of the Y row (n x 2, streamed from HBM) with the
-//     slice's (U,V) matrix in LDS;
-//   * lane t-1 hands mu_{i,t-1}^new to lane t through {epoch,value} granules
-//     (no fence on the critical path);
-//   * the d x d system is solved by Gauss-Jordan in fp64 in LDS;
-//   * every AME_SNAP_NB nodes the statistics are snapshotted so the
-//     covariance kernel can rebuild bit-identical precisions in parallel.
+// OLD means of nodes j>i at t and of node i at t+1: a 2-D wavefront.
+//
+// Design:
+//  * one workgroup per time slice ("lane" t), all lanes co-resident; lane t-1
+//    hands mu_{i,t-1}^new to lane t through {epoch,value} granules;
+//  * the lane keeps its slice's (U,V) in LDS for the GEMV h_obs = Z_i . [V|U];
+//  * no factorisation per step.  With F_j = J_j^T R^-1 J_j (J_j = [[1,0,V_j,0],
+//    [0,1,0,U_j]]) the precision of node i is
+//        P_i = P_const(t) + sum_{j != i} F_j(current),
+//    so consecutive precisions differ by rank 4.  The lane keeps
+//        K_i = (P_i - F_{i-1}(new))^-1                      (fp64, LDS)
+//    and per step (Woodbury):
+//        W = K J_{i-1}^T, M = R + J_{i-1} W, u = K g   (g = h minus node i-1's part)
+//        mu_i = u + W M^-1 (y_{i,i-1} - J_{i-1} u)      (= P_i^-1 h_i)
+//        P_i^-1 = K - W M^-1 W^T                         (-> X_cov output)
+//        K_{i+1} = P_i^-1 downdated by F_{i+1}(old)      (second rank-2 Woodbury)
+//    K_0 = P_0^-1 comes from one in-place sweep-operator inversion per sweep.
+//    Lower triangles are computed and mirrored, so K and every covariance are
+//    exactly symmetric (the reference's (C+C^T)/2 is an identity).
+//  * phases per step (3 workgroup barriers):
+//      1 all   : K-matvecs (W, Y' = K J_{i+1}^T, u) ; stage z row of node i+1
+//      2 wave 0: reductions, 2x2 solves, mu_i, publish ;
+//        waves 1-3: GEMV for node i+1, poll mu_{i+1,t-1}, load mu_{i+1,t+1}
+//      3 all   : K rank-4 update + covariance write ; AR terms of node i+1
 #include "ame_common.h"
 
 #ifdef AME_STAMPS
 // Diagnostic build only (cdna_hip_programming.md §7, in-kernel stamps): lane
-// AME_STAMP_LANE records s_memtime after each phase for nodes
+// T_local/2 records s_memtime after each phase for nodes
 // [AME_STAMP_I0, AME_STAMP_I0 + 16).  Never compiled into the product library.
 #define AME_STAMP_I0 256
-#define AME_STAMP_NPH 8
+#define AME_STAMP_NPH 16
 __device__ unsigned long long g_ame_stamps[16 * AME_STAMP_NPH];
-#define STAMP(ph)                                                                          \
+#define STAMP(ph) STAMPW(ph, 0)
+#define STAMPW(ph, who)                                                                    \
     do {                                                                                   \
-        if (stamp_on && tid == 0) {                                                        \
+        if (stamp_on && tid == (who)) {                                                    \
             unsigned long long t_;                                                         \
             __builtin_amdgcn_sched_barrier(0);                                             \
             asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");     \
@@ -47,61 +59,195 @@ extern "C" int ame_debug_read_stamps(unsigned long long* host, int count) {
 #define STAMP(ph) \
     do {          \
     } while (0)
+#define STAMPW(ph, who) \
+    do {                \
+    } while (0)
 #endif
+
+#define AME_YPF 8   // Y-row prefetch registers per thread (n <= 2048 fully prefetched)
+
+// Workgroup barrier that orders LDS only.  __syncthreads() lowers to a release
+// fence that waits vmcnt(0), exposing every in-flight prefetch load and every
+// covariance store at each barrier; here global traffic stays in flight across
+// phases (loads are waited for by the compiler at their first use; no other
+// wave of this workgroup reads what this kernel stores to global memory).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Wave-0 multi-dot: lanes k < D hold p[v]; every lane gets all NV sums.
+// Reduction: lane L sums red[v][part*QD .. +QD) (v = L>>2, part = L&3, QD =
+// ceil(D/4)), then a 4-lane xor reduction.  NV <= 16.
+template <int NV, int D>
+__device__ __forceinline__ void wave_multidot(const double (&pv)[NV], double (&out)[NV],
+                                              double* red /* 16*D */, double* sums, int lane) {
+    constexpr int QD = (D + 3) / 4;
+    if (lane < D) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) red[v * D + lane] = pv[v];
+    }
+    wave_lds_sync();
+    const int v = lane >> 2, part = lane & 3;
+    double acc = 0.0;
+    if (v < NV) {
+#pragma unroll
+        for (int k = 0; k < QD; ++k) {
+            const int kk = part * QD + k;
+            if (kk < D) acc += red[v * D + kk];
+        }
+    }
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    if (v < NV && part == 0) sums[v] = acc;
+    wave_lds_sync();
+#pragma unroll
+    for (int qq = 0; qq < NV; ++qq) out[qq] = sums[qq];
+    wave_lds_sync();
+}
+
+struct M22 {
+    double a, b, c, d;   // [[a b][c d]]
+};
+__device__ __forceinline__ M22 inv22(M22 m) {
+    const double id = 1.0 / (m.a * m.d - m.b * m.c);
+    return {m.d * id, -m.b * id, -m.c * id, m.a * id};
+}
+
+// lower-triangle index e -> (k, m), m <= k
+__device__ __forceinline__ void tri_decode(int e, int& k, int& m) {
+    k = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+    if ((k + 1) * (k + 2) / 2 <= e) ++k;
+    if (k * (k + 1) / 2 > e) --k;
+    m = e - k * (k + 1) / 2;
+}
 
 template <int R>
 __global__ void __launch_bounds__(AME_NT)
 ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
-    using C = AmeCfg<R>;
-    constexpr int D = C::D, M2 = C::M2, NS = C::NS, VEC = C::VEC, CW = C::CW, G = C::G,
-                  PW = C::PW, W = C::W, QN = C::QN, MC = C::MC;
+    constexpr int D = 2 + 2 * R, M2 = 2 * R, KS = D + 1, US = (M2 + 15) / 16;
+    constexpr int VEC = (R % 4 == 0) ? 4 : ((R % 2 == 0) ? 2 : 1);
+    constexpr int CW = M2 / VEC, GW = 192 / CW, PW = M2 + 2;
+    constexpr int MC = (D + 3) / 4;
+    constexpr int NLT = D * (D + 1) / 2, LTQ = (NLT + AME_NT - 1) / AME_NT;
     const int n = dm.n, TL = dm.T_local, Tt = dm.T_total;
     const int tl = blockIdx.x, tg = dm.t_begin + tl;
-    const int tid = threadIdx.x;
-    const int variant = dm.variant;
-    const int nblk = (n + AME_SNAP_NB - 1) / AME_SNAP_NB;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const bool is_naive = dm.variant == AME_NAIVE, is_bad = dm.variant == AME_BAD;
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const SweepLds L = sweep_lds_layout(n, R);
-    double* S = (double*)(smem + L.oS);
-    double* A = (double*)(smem + L.oA);
-    double* vh = (double*)(smem + L.oVh);
-    double* var = (double*)(smem + L.oVar);
-    float* mu_prev = (float*)(smem + L.oF);
-    float* mu_next = mu_prev + D;
-    float* mu_old = mu_next + D;
-    float* mu_new = mu_old + D;
-    float* part = (float*)(smem + L.oPart);
-    float2* z = (float2*)(smem + L.oZ);
-    float* M = (float*)(smem + L.oM);
+    double* K = (double*)(smem + L.oK);          // D x KS
+    double* vec = (double*)(smem + L.oVec);      // (5+US) x D  K-matvec results
+    double* upd = (double*)(smem + L.oUpd);      // 8 x D       rank-4 update vectors
+    double* red = (double*)(smem + L.oRed);      // 16 x D      wave-0 reduction scratch
+    double* scal = (double*)(smem + L.oScal);    // 64          sums / y_{i+1,i}
+    double* gobs = (double*)(smem + L.oG);       // D           g_obs of the current node
+    double* ar = gobs + D;                       // D           AR terms of the current node
+    double* ssq = (double*)(smem + L.oSsq);      // 2R          sum U^2, sum V^2 (naive diag)
+    double* pcd = ssq + 2 * R;                   // D           diag of P_const
+    float* mu_prev = (float*)(smem + L.oF);      // mu_{i-1,t}^new (becomes mu_i in phase 2)
+    float* mu_left = mu_prev + D;                // mu_{i+1,t-1}^new
+    float* mu_right = mu_prev + 2 * D;           // mu_{i+1,t+1}^old
+    float* mu_old = mu_prev + 3 * D;             // mu_{i,t}^old
+    float* mu_old_n = mu_prev + 4 * D;           // mu_{i+1,t}^old
+    float* part = (float*)(smem + L.oPart);      // GW x PW   GEMV partials
+    float2* z = (float2*)(smem + L.oZ);          // n         z row of the next node
+    float* M = (float*)(smem + L.oM);            // n x 2R    (U,V) of the slice
 
-    const double p = a.rinv[0], s = a.rinv[3];
-    const double q = 0.5 * (a.rinv[1] + a.rinv[2]);
-    const float r00 = (float)a.rinv[0], r01 = (float)a.rinv[1], r10 = (float)a.rinv[2],
-                r11 = (float)a.rinv[3];
-    const double nm1 = (double)(n - 1);
-
-    // ---- slice state: (U,V) of all nodes, then fp64 statistics ----
+    const double p = a.rinv[0], s = a.rinv[3], q = 0.5 * (a.rinv[1] + a.rinv[2]);
+    const double r00 = a.rinv[0], r01 = a.rinv[1], r10 = a.rinv[2], r11 = a.rinv[3];
+    const float r00f = (float)r00, r01f = (float)r01, r10f = (float)r10, r11f = (float)r11;
+    M22 Rm;   // R = R_inv^-1, symmetrised
+    {
+        Rm = inv22(M22{r00, r01, r10, r11});
+        Rm.b = Rm.c = 0.5 * (Rm.b + Rm.c);
+    }
+    const size_t DD = (size_t)D * D;
     const float* xo = a.x_old + (size_t)tl * n * D;
+    float* xn = a.x_new + (size_t)tl * n * D;
+    float* cvs = a.cov + (size_t)tl * n * DD;
+    const float* ysl = a.Yt + (size_t)tl * n * n * 2;
+    const float lr = a.lr, om = a.one_minus_lr;
+    bool dead = false;
+
+    // ------------------------------------------------------------------
+    // init: slice state, P_0 = P_const + sum_{j != 0} F_j, K_0 = P_0^-1
+    // ------------------------------------------------------------------
     for (int idx = tid; idx < n * M2; idx += AME_NT) {
         const int j = idx / M2, c = idx - j * M2;
         M[idx] = xo[(size_t)j * D + 2 + c];
     }
-    // constant precision entries owned by this thread (fixed for the slice)
-    double pc[QN];
-    int pk[QN], pm[QN];
-#pragma unroll
-    for (int qq = 0; qq < QN; ++qq) {
-        const int e = tid + AME_NT * qq;
-        pk[qq] = (e < D * D) ? e / D : 0;
-        pm[qq] = (e < D * D) ? e - (e / D) * D : 0;
-        pc[qq] = (e < D * D) ? pconst_entry(a.consts, D, pk[qq], pm[qq], tg, Tt) : 0.0;
+    if (tid < D) pcd[tid] = pconst_entry(a.consts, D, tid, tid, tg, Tt);
+    __syncthreads();
+    if (tid < M2) {   // sum of squares over all nodes: ssq[c<R] = sum U_c^2, ssq[R+c] = sum V_c^2
+        double acc = 0.0;
+        for (int j = 0; j < n; ++j) {
+            const double v = (double)M[j * M2 + tid];
+            acc = fma(v, v, acc);
+        }
+        ssq[tid] = acc;
     }
-    // AR rows: thread (k = tid>>2, part = tid&3) owns columns [part*MC, part*MC+MC)
-    double qiphi[MC], phitqi[MC];
+    for (int e = tid; e < NLT; e += AME_NT) {
+        int k, m;
+        tri_decode(e, k, m);
+        double v;
+        if (k < 2) {
+            v = ((k == 0 && m == 0) ? p : (k == 1 && m == 1) ? s : q) * (double)(n - 1);
+        } else {
+            const int ck = k - 2;
+            const bool ku = ck < R;                 // row U_ck: J entry V ; row V: J entry U
+            const int kc = ku ? R + ck : ck - R;
+            double acc = 0.0;
+            if (m < 2) {
+                for (int j = 1; j < n; ++j) acc += (double)M[j * M2 + kc];
+                v = (ku ? (m == 0 ? p : q) : (m == 0 ? q : s)) * acc;
+            } else {
+                const int cm = m - 2;
+                const bool mu_ = cm < R;
+                const int mc = mu_ ? R + cm : cm - R;
+                for (int j = 1; j < n; ++j)
+                    acc = fma((double)M[j * M2 + kc], (double)M[j * M2 + mc], acc);
+                v = ((ku && mu_) ? p : ((!ku && !mu_) ? s : q)) * acc;
+            }
+        }
+        v += pconst_entry(a.consts, D, k, m, tg, Tt);
+        K[k * KS + m] = v;
+        K[m * KS + k] = v;
+    }
+    __syncthreads();
+    for (int pv = 0; pv < D; ++pv) {   // in-place symmetric sweep: K -> -P_0^-1
+        if (tid < D) red[tid] = K[pv * KS + tid];
+        __syncthreads();
+        const double rinv = 1.0 / red[pv];
+        for (int e = tid; e < NLT; e += AME_NT) {
+            int k, m;
+            tri_decode(e, k, m);
+            double v;
+            if (k == pv && m == pv) v = -rinv;
+            else if (k == pv) v = red[m] * rinv;
+            else if (m == pv) v = red[k] * rinv;
+            else v = K[k * KS + m] - (red[k] * red[m]) * rinv;
+            K[k * KS + m] = v;
+            K[m * KS + k] = v;
+        }
+        __syncthreads();
+    }
+    for (int e = tid; e < D * D; e += AME_NT) {
+        const int k = e / D, m = e - k * D;
+        K[k * KS + m] = -K[k * KS + m];
+    }
+
+    double qiphi[MC], phitqi[MC];   // AR rows: thread (k = tid>>2, part = tid&3)
     {
         const int k = tid >> 2, pp = tid & 3;
-        const size_t DD = (size_t)D * D;
 #pragma unroll
         for (int mm = 0; mm < MC; ++mm) {
             const int m = pp * MC + mm;
@@ -110,220 +256,419 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             phitqi[mm] = ok ? a.consts[4 * DD + (size_t)k * D + m] : 0.0;
         }
     }
-    __syncthreads();
-    for (int e = tid; e < NS; e += AME_NT) {
-        double acc = 0.0;
-        for (int j = 0; j < n; ++j) acc = __dadd_rn(acc, stat_val<R>(e, M + j * M2, M + j * M2 + R));
-        S[e] = acc;
-    }
-    // Gauss-Jordan work split (compile-time stride W)
-    constexpr int GJ_PER = (D * W + AME_NT - 1) / AME_NT;
-    int gk[GJ_PER], gm[GJ_PER];
+    int lk[LTQ], lm[LTQ];   // lower-triangle entries owned for the update / cov write
 #pragma unroll
-    for (int qq = 0; qq < GJ_PER; ++qq) {
+    for (int qq = 0; qq < LTQ; ++qq) {
         const int e = tid + AME_NT * qq;
-        gk[qq] = (e < D * W) ? e / W : -1;
-        gm[qq] = (e < D * W) ? e - (e / W) * W : -1;
+        int k = -1, m = -1;
+        if (e < NLT) tri_decode(e, k, m);
+        lk[qq] = k;
+        lm[qq] = m;
     }
-    const int ncol = D + ((variant == AME_BAD) ? 2 : 1);
-    bool dead = false;   // a spin timed out: stop waiting, finish the sweep
+
+    // ---- helpers ----
+    float2 ypf[AME_YPF];
+    auto prefetch_y = [&](int node) {   // Y row of `node` -> registers
+        const float2* yrow = (const float2*)(ysl + (size_t)node * n * 2);
+#pragma unroll
+        for (int r = 0; r < AME_YPF; ++r) {
+            const int j = tid + AME_NT * r;
+#ifdef AME_ABL_NOY
+            ypf[r] = make_float2((float)j, 0.f); (void)yrow;
+#else
+            ypf[r] = (j < n) ? yrow[j] : make_float2(0.f, 0.f);
+#endif
+        }
+    };
+    auto stage_z = [&](int node, int excl) {   // z row of `node` from ypf (+ tail loads)
+        auto put = [&](int j, float2 y) {
+            float z0 = r00f * y.x + r01f * y.y;
+            float z1 = r10f * y.x + r11f * y.y;
+            if (j == excl) {   // y_{node,node-1}: Woodbury observation of the next step
+                scal[40] = (double)y.x;
+                scal[41] = (double)y.y;
+            }
+            if (j == node || j == excl) { z0 = 0.f; z1 = 0.f; }
+            z[j] = make_float2(z0, z1);
+        };
+#pragma unroll
+        for (int r = 0; r < AME_YPF; ++r) {
+            const int j = tid + AME_NT * r;
+            if (j < n) put(j, ypf[r]);
+        }
+        const float2* yrow = (const float2*)(ysl + (size_t)node * n * 2);
+        for (int j = tid + AME_NT * AME_YPF; j < n; j += AME_NT) put(j, yrow[j]);
+    };
+    auto gemv = [&](int tw) {   // partial h_obs over node group (waves 1-3: tw < 192)
+        const int g = tw / CW, cq = tw - g * CW;
+        if (g < GW) {
+            const int c0 = cq * VEC;
+            const bool upart = c0 < R;
+            const int mo = upart ? (R + c0) : (c0 - R);
+            float acc[VEC];
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) acc[v] = 0.f;
+            float s0 = 0.f, s1 = 0.f;
+#pragma unroll 4
+            for (int j = g; j < n; j += GW) {
+                const float2 zz = z[j];
+                const float zc = upart ? zz.x : zz.y;
+                const float* mr = M + j * M2 + mo;
+                if constexpr (VEC == 4) {
+                    const float4 mv = *(const float4*)mr;
+                    acc[0] = fmaf(zc, mv.x, acc[0]);
+                    acc[1] = fmaf(zc, mv.y, acc[1]);
+                    acc[2] = fmaf(zc, mv.z, acc[2]);
+                    acc[3] = fmaf(zc, mv.w, acc[3]);
+                } else if constexpr (VEC == 2) {
+                    const float2 mv = *(const float2*)mr;
+                    acc[0] = fmaf(zc, mv.x, acc[0]);
+                    acc[1] = fmaf(zc, mv.y, acc[1]);
+                } else {
+                    acc[0] = fmaf(zc, mr[0], acc[0]);
+                }
+                s0 += zz.x;
+                s1 += zz.y;
+            }
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) part[g * PW + c0 + v] = acc[v];
+            if (cq == 0) {
+                part[g * PW + M2] = s0;
+                part[g * PW + M2 + 1] = s1;
+            }
+        }
+    };
+    auto gemv_reduce = [&]() {   // threads < PW -> gobs
+        if (tid < PW) {
+            float acc = 0.f;
+            for (int g = 0; g < GW; ++g) acc += part[g * PW + tid];
+            gobs[(tid < M2) ? 2 + tid : tid - M2] = (double)acc;
+        }
+    };
+    auto ar_terms = [&]() {   // threads < 4D: ar = QiPhi mu_left + PhiTQi mu_right
+        if (tid < 4 * D) {
+            const int k = tid >> 2, pp = tid & 3;
+            double acc = 0.0;
+#pragma unroll
+            for (int mm = 0; mm < MC; ++mm) {
+                const int m = pp * MC + mm;
+                if (m < D) {
+                    if (tg > 0) acc = fma(qiphi[mm], (double)mu_left[m], acc);
+                    if (tg < Tt - 1) acc = fma(phitqi[mm], (double)mu_right[m], acc);
+                }
+            }
+            acc += __shfl_xor(acc, 1);
+            acc += __shfl_xor(acc, 2);
+            if (pp == 0) ar[k] = acc;
+        }
+    };
+    // wave 1: issue the granule loads of mu_{node,t-1}^new (returns when done or timed out)
+    auto poll_left = [&](int node, uint64_t first) {
+        const int k = lane;
+        const bool from_halo = (tl == 0);
+        const uint64_t* src = from_halo ? a.halo_in + (size_t)node * D
+                                        : a.hand + ((size_t)(tl - 1) * n + node) * D;
+        uint64_t v = first;
+        bool ok = (k >= D) || (uint32_t)(v >> 32) == a.epoch;
+        if (!__all(ok) && !dead) {
+            const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+            const uint64_t budget = from_halo ? AME_SPIN_TICKS_HALO : AME_SPIN_TICKS_LOCAL;
+            while (true) {
+                __builtin_amdgcn_s_sleep(2);
+                if (k < D) {
+                    v = from_halo ? gran_load_system(src + k) : gran_load_agent(src + k);
+                    ok = (uint32_t)(v >> 32) == a.epoch;
+                }
+                if (__all(ok)) break;
+                if (__builtin_amdgcn_s_memrealtime() - t_start > budget) {
+                    if (k == 0)
+                        atomicOr(a.status, from_halo ? AME_STATUS_HALO_TIMEOUT
+                                                     : AME_STATUS_SPIN_TIMEOUT);
+                    dead = true;
+                    break;
+                }
+            }
+        }
+        if (k < D) mu_left[k] = __uint_as_float((uint32_t)v);
+    };
+    auto first_poll = [&](int node) -> uint64_t {   // wave 1: issue the first granule loads
+        if (tg == 0 || lane >= D) return 0;
+        const bool from_halo = (tl == 0);
+        const uint64_t* src = from_halo ? a.halo_in + (size_t)node * D
+                                        : a.hand + ((size_t)(tl - 1) * n + node) * D;
+        return from_halo ? gran_load_system(src + lane) : gran_load_agent(src + lane);
+    };
+    auto right_regs = [&](int node, float& nx, float& ol) {   // threads 128..128+D
+        const int k = tid - 128;
+        nx = 0.f;
+        if (tg < Tt - 1)
+            nx = (tl < TL - 1) ? a.x_old[((size_t)(tl + 1) * n + node) * D + k]
+                               : a.next_old[(size_t)node * D + k];
+        ol = xo[(size_t)node * D + k];
+    };
+
+    // ---- prologue: vectors, g_obs and AR of node 0 ----
+    prefetch_y(0);
+    {
+        float nx = 0.f, ol = 0.f;
+        if (tid >= 128 && tid < 128 + D) right_regs(0, nx, ol);
+        stage_z(0, -1);
+        if (wave == 1) {
+            if (tg > 0) poll_left(0, first_poll(0));
+            else if (lane < D) mu_left[lane] = 0.f;
+        }
+        if (tid >= 128 && tid < 128 + D) {
+            mu_right[tid - 128] = nx;
+            mu_old[tid - 128] = ol;
+        }
+    }
+    if (n > 1) prefetch_y(1);
+    __syncthreads();
+    if (wave >= 1) gemv(tid - 64);
+    __syncthreads();
+    gemv_reduce();
+    ar_terms();
     __syncthreads();
 
-    const float* yslice = a.Yt + (size_t)tl * n * n * 2;
-    float* xn = a.x_new + (size_t)tl * n * D;
-
+    float y_prev0 = 0.f, y_prev1 = 0.f;   // y_{i,i-1} (raw)
     for (int i = 0; i < n; ++i) {
 #ifdef AME_STAMPS
         const bool stamp_on = (tl == TL / 2) && i >= AME_STAMP_I0 && i < AME_STAMP_I0 + 16;
 #endif
         STAMP(0);
-        // (a) statistic snapshot for the covariance kernel
-        if ((i % AME_SNAP_NB) == 0) {
-            double* dst = a.snap + ((size_t)tl * nblk + i / AME_SNAP_NB) * NS;
-            for (int e = tid; e < NS; e += AME_NT) dst[e] = S[e];
-        }
-        // (b) z_ij = R^-1 y_ij for the Y row of node i (j == i masked)
+        const bool has_prev = i > 0, has_next = i + 1 < n;
+        float cold[LTQ], coldT[LTQ];   // old covariance of node i (used in phase 3)
         {
-            const float2* yrow = (const float2*)(yslice + (size_t)i * n * 2);
-            for (int j = tid; j < n; j += AME_NT) {
-                const float2 y = yrow[j];
-                float z0 = r00 * y.x + r01 * y.y;
-                float z1 = r10 * y.x + r11 * y.y;
-                if (j == i) { z0 = 0.f; z1 = 0.f; }
-                z[j] = make_float2(z0, z1);
+            const float* cv = cvs + (size_t)i * DD;
+#pragma unroll
+            for (int qq = 0; qq < LTQ; ++qq) {
+#ifdef AME_ABL_NOCOV
+                cold[qq] = 0.f; coldT[qq] = 0.f; (void)cv;
+#else
+                cold[qq] = (lk[qq] >= 0) ? cv[lk[qq] * D + lm[qq]] : 0.f;
+                coldT[qq] = (lk[qq] >= 0) ? cv[lm[qq] * D + lk[qq]] : 0.f;
+#endif
             }
         }
-        // (c) node vectors: old mean, right neighbour (old), left neighbour (new)
-        if (tid < D) {
-            mu_old[tid] = xo[(size_t)i * D + tid];
-            float nx = 0.f;
-            if (tg < Tt - 1)
-                nx = (tl < TL - 1) ? a.x_old[((size_t)(tl + 1) * n + i) * D + tid]
-                                   : a.next_old[(size_t)i * D + tid];
-            mu_next[tid] = nx;
+        // ---------------- phase 1 ----------------
+        if (has_prev && tid < M2) {   // node i-1: statistics and slice (U,V) <- new
+            const double vo = (double)M[(i - 1) * M2 + tid], vn = (double)mu_prev[2 + tid];
+            ssq[tid] = ssq[tid] - vo * vo + vn * vn;
+            M[(i - 1) * M2 + tid] = mu_prev[2 + tid];
         }
-        if (tg > 0) {
-            if (tid >= 64 && tid < 128) {   // wave 1 polls the hand-off granules
-                const int k = tid - 64;
-                const bool from_halo = (tl == 0);
-                const uint64_t* src = from_halo ? a.halo_in + (size_t)i * D
-                                                : a.hand + ((size_t)(tl - 1) * n + i) * D;
-                uint64_t v = 0;
-                const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-                const uint64_t budget = from_halo ? AME_SPIN_TICKS_HALO : AME_SPIN_TICKS_LOCAL;
-                while (true) {
-                    bool ok = true;
-                    if (k < D) {
-                        v = from_halo ? gran_load_system(src + k) : gran_load_agent(src + k);
-                        ok = (uint32_t)(v >> 32) == a.epoch;
-                    }
-                    if (__all(ok) || dead) break;
-                    if (__builtin_amdgcn_s_memrealtime() - t_start > budget) {
-                        if (k == 0)
-                            atomicOr(a.status, from_halo ? AME_STATUS_HALO_TIMEOUT
-                                                         : AME_STATUS_SPIN_TIMEOUT);
-                        dead = true;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(2);
-                }
-                if (k < D) mu_prev[k] = __uint_as_float((uint32_t)v);
-            }
-        } else if (tid < D) {
-            mu_prev[tid] = 0.f;
-        }
-        __syncthreads();   // B1
-        STAMP(1);
-
-        // (d) GEMV partials: h_U = sum_j z0_j V_j, h_V = sum_j z1_j U_j (+ sums of z)
         {
-            const int g = tid / CW, cq = tid - g * CW;
-            if (g < G) {
-                const int c0 = cq * VEC;
-                const bool upart = c0 < R;
-                const int mo = upart ? (R + c0) : (c0 - R);
-                float acc[VEC];
-#pragma unroll
-                for (int v = 0; v < VEC; ++v) acc[v] = 0.f;
-                float s0 = 0.f, s1 = 0.f;
-                for (int j = g; j < n; j += G) {
-                    const float2 zz = z[j];
-                    const float zc = upart ? zz.x : zz.y;
-                    const float* mr = M + j * M2 + mo;
-                    if constexpr (VEC == 4) {
-                        const float4 mv = *(const float4*)mr;
-                        acc[0] = fmaf(zc, mv.x, acc[0]);
-                        acc[1] = fmaf(zc, mv.y, acc[1]);
-                        acc[2] = fmaf(zc, mv.z, acc[2]);
-                        acc[3] = fmaf(zc, mv.w, acc[3]);
-                    } else if constexpr (VEC == 2) {
-                        const float2 mv = *(const float2*)mr;
-                        acc[0] = fmaf(zc, mv.x, acc[0]);
-                        acc[1] = fmaf(zc, mv.y, acc[1]);
-                    } else {
-                        acc[0] = fmaf(zc, mr[0], acc[0]);
-                    }
-                    s0 += zz.x;
-                    s1 += zz.y;
-                }
-#pragma unroll
-                for (int v = 0; v < VEC; ++v) part[g * PW + c0 + v] = acc[v];
-                if (cq == 0) {
-                    part[g * PW + M2] = s0;
-                    part[g * PW + M2 + 1] = s1;
-                }
-            }
-            // AR terms: Qinv Phi mu_{i,t-1}^new + Phi^T Qinv mu_{i,t+1}^old
-            if (tid < 4 * D) {
-                const int k = tid >> 2, pp = tid & 3;
+            constexpr int NIT = 4 * D + (1 + US) * D;
+            for (int it = tid; it < NIT; it += AME_NT) {
                 double acc = 0.0;
+                int slot, k;
+                if (it < 4 * D) {   // W0 W1 (node i-1 new) / Y0 Y1 (node i+1 old)
+                    k = it >> 2;
+                    const int qv = it & 3;
+                    slot = qv;
+                    const bool prevv = qv < 2;
+                    if (prevv ? has_prev : has_next) {
+                        const bool row0 = (qv & 1) == 0;   // e0 = [1,0,V,0] ; e1 = [0,1,0,U]
+                        const float* src = prevv ? (mu_prev + 2) : (M + (i + 1) * M2);
+                        const int cb = row0 ? 2 : 2 + R;
+                        const float* vv = row0 ? (src + R) : src;
+                        acc = K[k * KS + (row0 ? 0 : 1)];
 #pragma unroll
-                for (int mm = 0; mm < MC; ++mm) {
-                    const int m = pp * MC + mm;
-                    if (m < D) {
-                        if (tg > 0) acc = fma(qiphi[mm], (double)mu_prev[m], acc);
-                        if (tg < Tt - 1) acc = fma(phitqi[mm], (double)mu_next[m], acc);
+                        for (int c = 0; c < R; ++c) acc = fma(K[k * KS + cb + c], (double)vv[c], acc);
+                    }
+                } else if (it < 5 * D) {   // u, a-part
+                    k = it - 4 * D;
+                    slot = 4;
+                    acc = K[k * KS + 0] * (gobs[0] + ar[0]) + K[k * KS + 1] * (gobs[1] + ar[1]);
+                } else {                   // u, (U,V)-part chunk
+                    const int r2 = it - 5 * D, ch = r2 / D;
+                    k = r2 - ch * D;
+                    slot = 5 + ch;
+                    const int m0 = 2 + ch * 16, m1 = min(D, m0 + 16);
+                    for (int m = m0; m < m1; ++m) acc = fma(K[k * KS + m], gobs[m] + ar[m], acc);
+                }
+                vec[slot * D + k] = acc;
+            }
+            STAMPW(4, 0);
+            STAMPW(5, 128);
+            STAMPW(6, 192);
+            if (has_next) stage_z(i + 1, i);
+            STAMPW(7, 0);
+        }
+        lds_barrier();   // B1
+        STAMP(1);
+        // ---------------- phase 2 ----------------
+        if (wave == 0) {
+            const int k = lane;
+            const bool kl = k < D;
+            double W0 = 0, W1 = 0, Y0 = 0, Y1 = 0, ua = 0, uM = 0, gk = 0, K0 = 0, K1 = 0;
+            double jp0 = 0, jp1 = 0, jn0 = 0, jn1 = 0;
+            if (kl) {
+                W0 = vec[k]; W1 = vec[D + k]; Y0 = vec[2 * D + k]; Y1 = vec[3 * D + k];
+                ua = vec[4 * D + k];
+#pragma unroll
+                for (int ch = 0; ch < US; ++ch) uM += vec[(5 + ch) * D + k];
+                gk = gobs[k] + ar[k];
+                K0 = K[k * KS + 0];
+                K1 = K[k * KS + 1];
+                if (k == 0) { jp0 = 1.0; jn0 = 1.0; }
+                if (k == 1) { jp1 = 1.0; jn1 = 1.0; }
+                if (k >= 2 && k < 2 + R) {
+                    jp0 = (double)mu_prev[2 + R + (k - 2)];
+                    if (has_next) jn0 = (double)M[(i + 1) * M2 + R + (k - 2)];
+                }
+                if (k >= 2 + R) {
+                    jp1 = (double)mu_prev[2 + (k - 2 - R)];
+                    if (has_next) jn1 = (double)M[(i + 1) * M2 + (k - 2 - R)];
+                }
+            }
+            const double u = ua + uM;
+            const double z0 = r00 * (double)y_prev0 + r01 * (double)y_prev1;
+            const double z1 = r10 * (double)y_prev0 + r11 * (double)y_prev1;
+            const double hk = has_prev ? gk + jp0 * z0 + jp1 * z1 : gk;   // natural parameter
+            double mus;
+            double Lp0 = 0, Lp1 = 0, Rp0 = 0, Rp1 = 0;   // P_i^-1 = K - Lp Rp^T
+            double Xp0 = Y0, Xp1 = Y1;                   // X' = P_i^-1 J_{i+1}^T
+            if (has_prev) {
+                double pr[14], o[14];
+                pr[0] = jp0 * W0; pr[1] = jp0 * W1; pr[2] = jp1 * W0; pr[3] = jp1 * W1;
+                pr[4] = jp0 * u;  pr[5] = jp1 * u;
+                pr[6] = jp0 * Y0; pr[7] = jp0 * Y1; pr[8] = jp1 * Y0; pr[9] = jp1 * Y1;
+                pr[10] = jp0 * ua; pr[11] = jp1 * ua; pr[12] = jp0 * uM; pr[13] = jp1 * uM;
+                wave_multidot<14, D>(pr, o, red, scal, lane);
+                STAMPW(8, 0);
+                M22 Mm = {Rm.a + o[0], Rm.b + 0.5 * (o[1] + o[2]), 0.0, Rm.d + o[3]};
+                Mm.c = Mm.b;
+                M22 Mi = inv22(Mm);
+                Mi.b = Mi.c = 0.5 * (Mi.b + Mi.c);
+                const double wm0 = W0 * Mi.a + W1 * Mi.c, wm1 = W0 * Mi.b + W1 * Mi.d;
+                Lp0 = wm0; Lp1 = wm1; Rp0 = W0; Rp1 = W1;
+                if (!is_bad) {
+                    mus = u + wm0 * ((double)y_prev0 - o[4]) + wm1 * ((double)y_prev1 - o[5]);
+                } else {
+                    // P^-1 h^(x) = K h^(x) - W M^-1 (J K h^(x)); J K[:,b] = (W0[b], W1[b])
+                    const double Wa00 = __shfl(W0, 0), Wa01 = __shfl(W0, 1);
+                    const double Wa10 = __shfl(W1, 0), Wa11 = __shfl(W1, 1);
+                    const double ta = ua + z0 * K0 + z1 * K1;
+                    const double tM = uM + z0 * (W0 - K0) + z1 * (W1 - K1);
+                    if (k < 2) {
+                        const double j0 = o[10] + z0 * Wa00 + z1 * Wa01;
+                        const double j1 = o[11] + z0 * Wa10 + z1 * Wa11;
+                        mus = ta - (wm0 * j0 + wm1 * j1);
+                    } else {
+                        const double j0 = o[12] + z0 * (o[0] - Wa00) + z1 * (o[1] - Wa01);
+                        const double j1 = o[13] + z0 * (o[2] - Wa10) + z1 * (o[3] - Wa11);
+                        mus = tM - (wm0 * j0 + wm1 * j1);
                     }
                 }
-                acc += __shfl_xor(acc, 1);
-                acc += __shfl_xor(acc, 2);
-                if (pp == 0) var[k] = acc;
-            }
-        }
-        __syncthreads();   // B2
-        STAMP(2);
-
-        // (e) natural parameter (reduce partials) and augmented precision [P | rhs]
-        if (tid < PW) {
-            float acc = 0.f;
-            for (int g = 0; g < G; ++g) acc += part[g * PW + tid];
-            const int kk = (tid < M2) ? 2 + tid : tid - M2;
-            const double h = (double)acc + var[kk];
-            vh[kk] = h;
-            if (variant == AME_BAD) {
-                A[kk * W + D] = (kk < 2) ? h : 0.0;
-                A[kk * W + D + 1] = (kk < 2) ? 0.0 : h;
+                Xp0 = Y0 - (wm0 * o[6] + wm1 * o[8]);
+                Xp1 = Y1 - (wm0 * o[7] + wm1 * o[9]);
             } else {
-                A[kk * W + D] = h;
+                mus = is_bad ? ((k < 2) ? ua : uM) : u;
+            }
+            if (!is_naive) mus += 1e-6 * hk;
+            if (kl) {   // damped new mean; publish (mu_prev: readers above are done, wave-ordered)
+                const float nw = __fadd_rn(__fmul_rn(lr, (float)mus), __fmul_rn(om, mu_old[k]));
+                xn[(size_t)i * D + k] = nw;
+                mu_prev[k] = nw;
+                const uint64_t g = ((uint64_t)a.epoch << 32) | (uint64_t)__float_as_uint(nw);
+                gran_store_agent(a.hand + ((size_t)tl * n + i) * D + k, g);
+                if (tl == TL - 1 && a.halo_out != nullptr)
+                    gran_store_system(a.halo_out + (size_t)i * D + k, g);
+            }
+            STAMPW(9, 0);
+            double Lm0 = 0, Lm1 = 0, Rm0 = 0, Rm1 = 0;   // downdate: + X' S'^-1 X'^T
+            if (has_next) {
+                double pr2[4], o2[4];
+                pr2[0] = jn0 * Xp0; pr2[1] = jn0 * Xp1; pr2[2] = jn1 * Xp0; pr2[3] = jn1 * Xp1;
+                wave_multidot<4, D>(pr2, o2, red, scal + 16, lane);
+                M22 Sm = {Rm.a - o2[0], Rm.b - 0.5 * (o2[1] + o2[2]), 0.0, Rm.d - o2[3]};
+                Sm.c = Sm.b;
+                M22 Si = inv22(Sm);
+                Si.b = Si.c = 0.5 * (Si.b + Si.c);
+                Lm0 = Xp0 * Si.a + Xp1 * Si.c;
+                Lm1 = Xp0 * Si.b + Xp1 * Si.d;
+                Rm0 = Xp0;
+                Rm1 = Xp1;
+            }
+            STAMPW(10, 0);
+            if (kl) {
+                upd[k] = Lp0; upd[D + k] = Lp1; upd[2 * D + k] = Rp0; upd[3 * D + k] = Rp1;
+                upd[4 * D + k] = Lm0; upd[5 * D + k] = Lm1; upd[6 * D + k] = Rm0; upd[7 * D + k] = Rm1;
+            }
+        } else if (has_next) {
+            // waves 1-3: next-node loads first (latency hidden by the GEMV), GEMV, then hand-offs
+            float nx = 0.f, ol = 0.f;
+            if (tid >= 128 && tid < 128 + D) right_regs(i + 1, nx, ol);
+            uint64_t g0 = 0;
+            if (wave == 1 && tg > 0) g0 = first_poll(i + 1);
+            if (i + 2 < n) prefetch_y(i + 2);
+            gemv(tid - 64);
+            STAMPW(11, 64);
+            STAMPW(13, 128);
+            if (wave == 1) {
+                if (tg > 0) poll_left(i + 1, g0);
+                else if (lane < D) mu_left[lane] = 0.f;
+                STAMPW(12, 64);
+            }
+            if (tid >= 128 && tid < 128 + D) {
+                mu_right[tid - 128] = nx;
+                mu_old_n[tid - 128] = ol;
             }
         }
+        if (wave == 0 && i + 2 < n && has_next) prefetch_y(i + 2);
+        lds_barrier();   // B2
+        STAMP(2);
+        // ---------------- phase 3 ----------------
         {
-            const float* Uo = M + i * M2;
-            const float* Vo = Uo + R;
+            float* cv = cvs + (size_t)i * DD;
 #pragma unroll
-            for (int qq = 0; qq < QN; ++qq) {
-                const int e = tid + AME_NT * qq;
-                if (e < D * D) {
-                    const double po = pobs_entry<R>(pk[qq], pm[qq], S, Uo, Vo, p, q, s, nm1);
-                    A[pk[qq] * W + pm[qq]] = __dadd_rn(po, pc[qq]);
+            for (int qq = 0; qq < LTQ; ++qq) {
+                const int k = lk[qq], m = lm[qq];
+                if (k < 0) continue;
+                const double c = K[k * KS + m] - (upd[k] * upd[2 * D + m] + upd[D + k] * upd[3 * D + m]);
+                const double kn = c + (upd[4 * D + k] * upd[6 * D + m] + upd[5 * D + k] * upd[7 * D + m]);
+                K[k * KS + m] = kn;
+                K[m * KS + k] = kn;
+                float c32;
+                if (is_naive) {   // C = diag(1 / (diag(P_i) + 1e-8))  (naive_mf.py:271-274)
+                    c32 = 0.f;
+                    if (k == m) {
+                        double pd;
+                        if (k == 0) pd = p * (double)(n - 1);
+                        else if (k == 1) pd = s * (double)(n - 1);
+                        else if (k < 2 + R) {
+                            const double vo = (double)M[i * M2 + R + (k - 2)];
+                            pd = p * (ssq[R + (k - 2)] - vo * vo);
+                        } else {
+                            const double uo = (double)M[i * M2 + (k - 2 - R)];
+                            pd = s * (ssq[k - 2 - R] - uo * uo);
+                        }
+                        c32 = 1.0f / ((float)(pd + pcd[k]) + 1e-8f);
+                    }
+                } else {
+                    c32 = (float)c;
+                    if (is_bad && ((k < 2) != (m < 2))) c32 = 0.f;
+                    if (k == m) c32 = c32 + 1e-6f;
                 }
+#ifdef AME_ABL_NOCOV
+                if (c32 == 12345.f) cv[0] = c32 + cold[qq] + coldT[qq];
+#else
+                cv[k * D + m] = __fadd_rn(__fmul_rn(lr, c32), __fmul_rn(om, cold[qq]));
+                if (k != m) cv[m * D + k] = __fadd_rn(__fmul_rn(lr, c32), __fmul_rn(om, coldT[qq]));
+#endif
             }
+            STAMPW(14, 0);
+            if (has_next) {
+                gemv_reduce();
+                ar_terms();
+            }
+            STAMPW(15, 0);
+            if (tid >= 128 && tid < 128 + D) mu_old[tid - 128] = mu_old_n[tid - 128];
+            y_prev0 = (float)scal[40];
+            y_prev1 = (float)scal[41];
         }
-        __syncthreads();   // B3
+        lds_barrier();   // B3
         STAMP(3);
-
-        // (f) Gauss-Jordan elimination (SPD: no pivoting), fp64
-        for (int pv = 0; pv < D; ++pv) {
-            const double pinv = 1.0 / A[pv * W + pv];
-#pragma unroll
-            for (int qq = 0; qq < GJ_PER; ++qq) {
-                const int k = gk[qq], m = gm[qq];
-                if (k >= 0 && k != pv && m > pv && m < ncol) {
-                    const double f = A[k * W + pv] * pinv;
-                    A[k * W + m] = fma(-f, A[pv * W + m], A[k * W + m]);
-                }
-            }
-            __syncthreads();
-        }
-
-        STAMP(4);
-        // (g) new mean: mu* = C h with C = sym(P^-1) (+1e-6 I), damped
-        if (tid < D) {
-            const int k = tid;
-            const int col = (variant == AME_BAD && k >= 2) ? D + 1 : D;
-            double x = A[k * W + col] / A[k * W + k];
-            if (variant != AME_NAIVE) x += 1e-6 * vh[k];
-            const float mu = (float)x;
-            const float nw = __fadd_rn(__fmul_rn(a.lr, mu), __fmul_rn(a.one_minus_lr, mu_old[k]));
-            mu_new[k] = nw;
-            xn[(size_t)i * D + k] = nw;
-            const uint64_t gv = ((uint64_t)a.epoch << 32) | (uint64_t)__float_as_uint(nw);
-            gran_store_agent(a.hand + ((size_t)tl * n + i) * D + k, gv);
-            if (tl == TL - 1 && a.halo_out != nullptr)
-                gran_store_system(a.halo_out + (size_t)i * D + k, gv);
-        }
-        __syncthreads();   // B4
-        STAMP(5);
-
-        // (h) statistics: S += stat(new) - stat(old)
-        {
-            const float* Uo = M + i * M2;
-            for (int e = tid; e < NS; e += AME_NT)
-                S[e] = stat_apply<R>(S[e], e, mu_new + 2, mu_new + 2 + R, Uo, Uo + R);
-        }
-        __syncthreads();   // B5
-        STAMP(6);
-        if (tid < M2) M[i * M2 + tid] = mu_new[2 + tid];
     }
 }
 

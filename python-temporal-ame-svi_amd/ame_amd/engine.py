@@ -7,13 +7,12 @@ One engine per process / GPU.  It owns, for the local time slices
     x_a, x_b  [T_local][n][d]    fp32   means, ping-pong (old / new of a sweep)
     cov       [T_local][n][d][d] fp32   covariances, updated in place
     hand      [T_local][n][d]    u64    lane-to-lane {epoch,value} granules
-    snap      [T_local][n/16][2r+3r^2] fp64 sweep statistic snapshots
     cov_terms [T_local][n][4]    fp64   per-(node,time) covariance ELBO terms
 
 and runs, per fit() iteration (reference base.py:170-181):
 
-    ame_sweep   (means; _update_step)       structured_mf.py:211-326
-    ame_cov     (covariances + cov terms)   structured_mf.py:266-287, 202-209
+    ame_sweep   (means + covariances)       structured_mf.py:211-326
+    ame_cov     (covariance ELBO terms)     structured_mf.py:142-144, 166, 193, 202-209
     ame_elbo    (pair + node sums)          structured_mf.py:115-200, temporal_ame.py:255-291
 
 The host then assembles ELBO and MSE from 8 fp64 sums (+ the analytic
@@ -31,7 +30,6 @@ import torch
 from . import _lib
 
 LOG2PI = math.log(2.0 * math.pi)
-SNAP_NB = 16
 VARIANTS = {"good": _lib.AME_GOOD, "bad": _lib.AME_BAD, "naive": _lib.AME_NAIVE}
 
 
@@ -144,10 +142,7 @@ class DeviceEngine:
             self.x_b = torch.empty_like(self.x_a)
             self.cov = X_cov[:, t0:t1].detach().float().permute(1, 0, 2, 3).contiguous().to(dev)
             n, d, TL = self.n, self.d, sh.T_local
-            nblk = (n + SNAP_NB - 1) // SNAP_NB
-            ns = 2 * self.r + 3 * self.r * self.r
             self.hand = torch.zeros(TL * n * d, dtype=torch.int64, device=dev)
-            self.snap = torch.empty(TL * nblk * ns, dtype=torch.float64, device=dev)
             self.cov_terms = torch.zeros(TL * n * 4, dtype=torch.float64, device=dev)
             ws = int(self.L.ame_elbo_work_size(ctypes.byref(self.dims)))
             if ws < 0:
@@ -218,21 +213,15 @@ class DeviceEngine:
             next_old, halo_in, halo_out = self.halo.before_sweep(self)
         a = _lib.ame_sweep_args(
             Yt=_ptr(self.Yt), x_old=_ptr(self.x_a), x_new=_ptr(self.x_b), next_old=next_old,
-            hand=_ptr(self.hand), halo_in=halo_in, halo_out=halo_out, snap=_ptr(self.snap),
+            hand=_ptr(self.hand), halo_in=halo_in, halo_out=halo_out, cov=_ptr(self.cov),
             consts=_ptr(self.consts), rinv=self.C.rinv4(), lr=self.lr,
             one_minus_lr=float(1.0 - self.lr), epoch=self.epoch, status=_ptr(self.status))
         tok = self._tic("sweep")
         _lib.check(self.L.ame_sweep(ctypes.byref(self.dims), ctypes.byref(a), self._sp()),
                    "ame_sweep")
         self._toc(tok)
-        c = _lib.ame_cov_args(
-            x_old=_ptr(self.x_a), x_new=_ptr(self.x_b), cov=_ptr(self.cov), snap=_ptr(self.snap),
-            consts=_ptr(self.consts), cov_terms=_ptr(self.cov_terms), rinv=self.C.rinv4(),
-            lr=self.lr, one_minus_lr=float(1.0 - self.lr), update=1)
-        tok = self._tic("cov")
-        _lib.check(self.L.ame_cov(ctypes.byref(self.dims), ctypes.byref(c), self._sp()), "ame_cov")
-        self._toc(tok)
         self.x_a, self.x_b = self.x_b, self.x_a
+        self.refresh_cov_terms()
         self._out_valid = False
         self._cov_terms_valid = True
         if self.halo is not None:
@@ -240,11 +229,11 @@ class DeviceEngine:
 
     def refresh_cov_terms(self):
         """Covariance ELBO terms of the current covariances (no update)."""
-        c = _lib.ame_cov_args(
-            x_old=_ptr(self.x_a), x_new=_ptr(self.x_a), cov=_ptr(self.cov), snap=None,
-            consts=_ptr(self.consts), cov_terms=_ptr(self.cov_terms), rinv=self.C.rinv4(),
-            lr=self.lr, one_minus_lr=float(1.0 - self.lr), update=0)
+        c = _lib.ame_cov_args(cov=_ptr(self.cov), consts=_ptr(self.consts),
+                              cov_terms=_ptr(self.cov_terms))
+        tok = self._tic("cov")
         _lib.check(self.L.ame_cov(ctypes.byref(self.dims), ctypes.byref(c), self._sp()), "ame_cov")
+        self._toc(tok)
         self._cov_terms_valid = True
 
     def launch_elbo(self):

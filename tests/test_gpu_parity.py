@@ -123,7 +123,11 @@ def test_single_node_update(gpu_device):
     (48, 6, 8, "naive", 0.3), (70, 5, 6, "good", 1.0), (40, 4, 16, "good", 0.01),
     (20, 1, 2, "good", 1.0), (2, 3, 2, "bad", 0.7), (24, 3, 7, "naive", 1.0)])
 def test_vs_oracle_fp64(n, T, r, method, lr, gpu_device):
-    """Random configurations (odd r, T=1, n=2, ...) against the fp64 oracle."""
+    """Random configurations (odd r, T=1, n=2, ...) against the fp64 oracle.
+
+    Bound: 5e-6 relative, or -- where the problem itself amplifies fp32
+    round-off (lr=1, larger r) -- no further from the fp64 oracle than the
+    reference's own fp32 arithmetic (the fp32 oracle) is."""
     import ame_oracle as O
     from ame_amd import TemporalAMEModel
     m = TemporalAMEModel(n, T, r, seed=7)
@@ -134,10 +138,15 @@ def test_vs_oracle_fp64(n, T, r, method, lr, gpu_device):
     params = {k: getattr(m, k).numpy().astype(np.float64)
               for k in ("R", "R_inv", "Sigma", "Psi", "Phi", "Q")}
     Y = m.Y.numpy().astype(np.float64)
+    Xm32 = vi.X_mean.numpy().copy()
+    Xc32 = vi.X_cov.numpy().copy()
     ref = O.fit(Y, Xm, Xc, params, method, lr, max_iter=2, tolerance=0.0)
+    p32 = {k: v.astype(np.float32) for k, v in params.items()}
+    O.fit(m.Y.numpy(), Xm32, Xc32, p32, method, lr, max_iter=2, tolerance=0.0)
+    fp32_err = np.abs(Xm32.astype(np.float64) - Xm).max()
     h = vi.fit(max_iter=2, tolerance=0.0, verbose=False)
     err = np.abs(vi.X_mean.numpy() - Xm).max()
-    assert err <= 5e-6 * max(1.0, np.abs(Xm).max()), err
+    assert err <= max(5e-6 * max(1.0, np.abs(Xm).max()), fp32_err), (err, fp32_err)
     cerr = np.abs(vi.X_cov.numpy() - Xc).max()
     assert cerr <= 1e-6 * max(1.0, np.abs(Xc).max()), cerr
     for a, b in zip(h["elbo"], ref["elbo"]):

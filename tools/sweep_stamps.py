@@ -15,26 +15,37 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "python-temporal-ame-svi_amd")
 BDIR = os.path.join(PKG, "ame_amd", "_build")
 SO = os.path.join(BDIR, "libame_amd_stamps.so")
-PHASES = ["snap+Yrow+vectors+poll", "GEMV+AR", "reduce+P build", "Gauss-Jordan",
-          "mu out+granules", "stats update", "M update (+next step start)"]
+PHASES = ["phase 1: K-matvecs + z staging", "phase 2: wave0 Woodbury | waves1-3 GEMV+poll",
+          "phase 3: K rank-4 update + cov write + AR", "loop (+ cov prefetch issue)"]
+
+
+def _opt(name, default=None):
+    for a in sys.argv:
+        if a.startswith(name + "="):
+            return a.split("=", 1)[1]
+    return default
 
 
 def build(r=16):
+    """--defs=A,B adds -DA -DB (ablation switches); --tag=X names the library."""
     os.makedirs(BDIR, exist_ok=True)
     csrc = os.path.join(PKG, "ame_amd", "csrc")
+    defs = [f"-D{d}" for d in (_opt("--defs") or "").split(",") if d]
+    tag = _opt("--tag", "")
+    so = SO.replace(".so", f"{tag}.so")
     objs = []
     for src in ("ame_sweep.hip", "ame_cov.hip", "ame_elbo.hip", "ame_capi.hip"):
-        o = os.path.join(BDIR, src.replace(".hip", "_stamps.o"))
+        o = os.path.join(BDIR, src.replace(".hip", f"_stamps{tag}.o"))
         subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17",
-                               "-DAME_STAMPS", f"-DAME_ONLY_R={r}", "-Wno-pass-failed", "-c",
-                               os.path.join(csrc, src), "-o", o])
+                               "-DAME_STAMPS", f"-DAME_ONLY_R={r}", *defs, "-Wno-pass-failed",
+                               "-c", os.path.join(csrc, src), "-o", o])
         objs.append(o)
-    subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", SO, *objs])
-    print("built", SO)
+    subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", so, *objs])
+    print("built", so)
 
 
 def run():
-    os.environ["AME_LIB_PATH"] = SO
+    os.environ["AME_LIB_PATH"] = SO.replace(".so", f"{_opt('--tag', '')}.so")
     sys.path.insert(0, PKG)
     import torch
     from ame_amd import TemporalAMEModel, TemporalAMEStructuredMFVI
@@ -47,21 +58,31 @@ def run():
     torch.cuda.synchronize()
     L = _lib.lib()
     L.ame_debug_read_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    buf = (ctypes.c_ulonglong * (16 * 8))()
-    assert L.ame_debug_read_stamps(buf, 16 * 8) == 0
-    rows = [[buf[k * 8 + p] for p in range(8)] for k in range(16)]
-    tot = [0.0] * 7
+    NPH = 16
+    buf = (ctypes.c_ulonglong * (16 * NPH))()
+    assert L.ame_debug_read_stamps(buf, 16 * NPH) == 0
+    rows = [[buf[k * NPH + p] for p in range(NPH)] for k in range(16)]
+    nph = len(PHASES)
+    tot = [0.0] * nph
     step = []
     for k in range(15):
         r, nxt = rows[k], rows[k + 1]
-        seq = r[:7] + [nxt[0]]
-        for p in range(7):
+        seq = r[:nph] + [nxt[0]]
+        for p in range(nph):
             tot[p] += seq[p + 1] - seq[p]
         step.append(nxt[0] - r[0])
     T = sum(tot)
     print(f"mean step {sum(step) / len(step):.0f} cycles (s_memtime ticks)")
     for name, t in zip(PHASES, tot):
-        print(f"  {name:32s} {t / 15:9.0f}  {100 * t / T:5.1f}%")
+        print(f"  {name:48s} {t / 15:9.0f}  {100 * t / T:5.1f}%")
+    sub = {4: "w0 matvec items done", 5: "w2 matvec items done", 6: "w3 matvec items done",
+           7: "w0 z staged", 8: "w0 multidot-1 done", 9: "w0 mean published",
+           10: "w0 multidot-2 done", 11: "w1 gemv done", 12: "w1 poll done",
+           13: "w2 gemv done", 14: "w0 K update + cov write done", 15: "w0 gemv_reduce+AR done"}
+    base = {4: 0, 5: 0, 6: 0, 7: 0, 8: 1, 9: 1, 10: 1, 11: 1, 12: 1, 13: 1, 14: 2, 15: 2}
+    for ph in sorted(sub):
+        d = sum(rows[k][ph] - rows[k][base[ph]] for k in range(15)) / 15
+        print(f"    +{d:8.0f} after phase start: {sub[ph]}")
 
 
 if __name__ == "__main__":
