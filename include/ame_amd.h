@@ -52,6 +52,7 @@ enum ame_variant { AME_GOOD = 0, AME_BAD = 1, AME_NAIVE = 2 };
 /* status word bits (device-written) */
 #define AME_STATUS_SPIN_TIMEOUT 1u
 #define AME_STATUS_HALO_TIMEOUT 2u
+#define AME_STATUS_LDS_TIMEOUT 4u   /* intra-workgroup hand-off timed out (internal error) */
 
 typedef struct ame_dims {
     int32_t n;        /* nodes */
@@ -79,6 +80,8 @@ typedef struct ame_sweep_args {
     float one_minus_lr;          /* (float)(1 - lr) computed in double on the host */
     uint32_t epoch;              /* sweep counter, >= 1, identical on every rank */
     uint32_t* status;            /* [1] error word */
+    double* work;                /* scratch, >= ame_sweep_work_size() doubles (per-slice base
+                                    inverse and column sums of squares) */
 } ame_sweep_args;
 
 typedef struct ame_cov_args {
@@ -112,6 +115,9 @@ int ame_pack_y(const float* Y, float* Yt, const ame_dims* dims,
  * reference node order exactly: step (i,t) sees new means of nodes j<i at t
  * and of node i at t-1, and old means of nodes j>i at t and of node i at t+1. */
 int ame_sweep(const ame_dims* dims, const ame_sweep_args* args, void* stream);
+
+/* Scratch doubles ame_sweep needs in args->work. */
+long long ame_sweep_work_size(const ame_dims* dims);
 
 /* Largest T_local ame_sweep can run with for (n, r) on this device, 0 if the
  * per-slice state does not fit one workgroup. */

@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("AME_LIB_PATH") or os.path.join(_HERE, "libame_amd.so"
 AME_GOOD, AME_BAD, AME_NAIVE = 0, 1, 2
 AME_STATUS_SPIN_TIMEOUT = 1
 AME_STATUS_HALO_TIMEOUT = 2
+AME_STATUS_LDS_TIMEOUT = 4
 
 c_int32 = ctypes.c_int32
 c_vp = ctypes.c_void_p
@@ -29,7 +30,8 @@ class ame_sweep_args(ctypes.Structure):
     _fields_ = [("Yt", c_vp), ("x_old", c_vp), ("x_new", c_vp), ("next_old", c_vp),
                 ("hand", c_vp), ("halo_in", c_vp), ("halo_out", c_vp), ("cov", c_vp),
                 ("consts", c_vp), ("rinv", ctypes.c_double * 4), ("lr", ctypes.c_float),
-                ("one_minus_lr", ctypes.c_float), ("epoch", ctypes.c_uint32), ("status", c_vp)]
+                ("one_minus_lr", ctypes.c_float), ("epoch", ctypes.c_uint32), ("status", c_vp),
+                ("work", c_vp)]
 
 
 class ame_cov_args(ctypes.Structure):
@@ -43,7 +45,7 @@ class ame_elbo_args(ctypes.Structure):
 
 
 # every symbol include/ame_amd.h declares (checked by tests/test_capi.py)
-EXPORTS = ("ame_pack_y", "ame_sweep", "ame_sweep_max_slices", "ame_sweep_lds_bytes", "ame_cov",
+EXPORTS = ("ame_pack_y", "ame_sweep", "ame_sweep_work_size", "ame_sweep_max_slices", "ame_sweep_lds_bytes", "ame_cov",
            "ame_elbo", "ame_elbo_work_size", "ame_host_register", "ame_host_unregister",
            "ame_supported_r", "ame_last_error", "ame_version")
 
@@ -62,6 +64,10 @@ def _declare(L):
     L.ame_elbo.argtypes = [P(ame_dims), P(ame_elbo_args), c_vp]
     L.ame_elbo_work_size.argtypes = [P(ame_dims)]
     L.ame_elbo_work_size.restype = ctypes.c_longlong
+    L.ame_debug_selftest.argtypes = [c_vp, c_vp]
+    L.ame_debug_selftest.restype = ctypes.c_int
+    L.ame_sweep_work_size.argtypes = [P(ame_dims)]
+    L.ame_sweep_work_size.restype = ctypes.c_longlong
     L.ame_supported_r.argtypes = [P(ctypes.c_int), ctypes.c_int]
     L.ame_host_register.argtypes = [c_vp, ctypes.c_ulonglong, P(c_vp)]
     L.ame_host_unregister.argtypes = [c_vp]

@@ -2,12 +2,17 @@
 // Argument validation lives here so a bad call fails loudly with a message
 // instead of faulting on the GPU.
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "ame_common.h"
 
 int ame_sweep_dispatch(const ame_dims*, const ame_sweep_args*, hipStream_t);
 int ame_sweep_blocks_per_cu(int n, int r);
+int ame_sweep3_dispatch(const ame_dims*, const ame_sweep_args*, hipStream_t);
+int ame_sweep3_supported(int n, int r);
+int ame_sweep3_blocks_per_cu(int n, int r);
+long long ame_sweep3_work_doubles(const ame_dims*);
 int ame_cov_dispatch(const ame_dims*, const ame_cov_args*, hipStream_t);
 int ame_elbo_dispatch(const ame_dims*, const ame_elbo_args*, hipStream_t);
 long long ame_elbo_work_doubles(const ame_dims*);
@@ -28,6 +33,14 @@ static bool r_supported(int r) {
 #undef X
         default: return false;
     }
+}
+
+// v3 (solver + helper waves, register-resident slice) whenever the slice fits
+// its register budget; AME_SWEEP_V2=1 forces the v2 kernel (A/B runs).
+static bool use_v3(int n, int r) {
+    const char* e = getenv("AME_SWEEP_V2");
+    if (e && e[0] && e[0] != '0') return false;
+    return ame_sweep3_supported(n, r) != 0;
 }
 
 static int check_dims(const ame_dims* d) {
@@ -93,13 +106,18 @@ long long ame_sweep_lds_bytes(int n, int r) {
 
 int ame_sweep_max_slices(int n, int r) {
     if (!r_supported(r)) return 0;
-    const long long lds = sweep_lds_layout(n, r).total;
-    if (lds > 163840) return 0;
+    const bool v3 = use_v3(n, r);
+    if (!v3 && sweep_lds_layout(n, r).total > 163840) return 0;
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    const int per_cu = ame_sweep_blocks_per_cu(n, r);
+    const int per_cu = v3 ? ame_sweep3_blocks_per_cu(n, r) : ame_sweep_blocks_per_cu(n, r);
     return per_cu * cus;
+}
+
+long long ame_sweep_work_size(const ame_dims* dims) {
+    if (check_dims(dims)) return -1;
+    return ame_sweep3_work_doubles(dims);
 }
 
 int ame_pack_y(const float* Y, float* Yt, const ame_dims* dims, unsigned long long* mismatch,
@@ -118,12 +136,14 @@ int ame_sweep(const ame_dims* dims, const ame_sweep_args* a, void* stream) {
         return fail("ame_sweep: t_begin=%d > 0 needs halo_in", dims->t_begin);
     if (dims->t_begin + dims->T_local < dims->T_total && !a->next_old)
         return fail("ame_sweep: rank does not hold T-1 and next_old is NULL");
-    const long long lds = sweep_lds_layout(dims->n, dims->r).total;
-    if (lds > 163840)
+    const bool v3 = use_v3(dims->n, dims->r);
+    if (!v3 && sweep_lds_layout(dims->n, dims->r).total > 163840)
         return fail("ame_sweep: slice state (n=%d, r=%d) exceeds one workgroup's LDS", dims->n, dims->r);
+    if (v3 && !a->work) return fail("ame_sweep: work is NULL");
     const int maxs = ame_sweep_max_slices(dims->n, dims->r);
     if (dims->T_local > maxs)
         return fail("ame_sweep: T_local=%d exceeds co-resident workgroups (%d)", dims->T_local, maxs);
+    if (v3) return launched(ame_sweep3_dispatch(dims, a, (hipStream_t)stream), "sweep3");
     return launched(ame_sweep_dispatch(dims, a, (hipStream_t)stream), "sweep");
 }
 

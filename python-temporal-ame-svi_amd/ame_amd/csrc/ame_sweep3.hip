@@ -1,0 +1,1085 @@
+// K1 (v3): latency-optimised Gauss-Seidel sweep of TemporalAMEStructuredMFVI /
+// TemporalAMENaiveMFVI on gfx950 -- new means AND new covariances of every
+// (node, time) step.
+//
+// Reference semantics (Alfieriek/Python-Temporal-AME-SVI):
+//   _update_step                structured_mf.py:211-218  (for i in range(n))
+//   _update_node_i              structured_mf.py:220-287  (for t in range(T))
+//   _compute_observation_terms  structured_mf.py:289-326
+//   naive variant               naive_mf.py:207-282
+// Step (i,t) reads the NEW means of nodes j<i at t and of node i at t-1 and the
+// OLD means of nodes j>i at t and of node i at t+1 (2-D wavefront).
+//
+// Design (the algebra is restated and checked on CPU in
+// tests/test_sweep_algebra.py):
+//  * one 512-thread workgroup per time slice ("lane" t), all co-resident;
+//    lane t-1 hands mu_{i,t-1}^new to lane t through {epoch,value} granules;
+//  * wave 0 = SOLVER.  The only work between node i-1's new mean and node i's
+//    is one d x 2r matvec with the fp64 base inverse B_i (rows in registers),
+//    one 20-value cross-lane reduction and 2x2 algebra:
+//       K_i  = B_i - L_{i-1} W_{i-1}^T + G_{i-1} X_{i-1}^T   (applied lazily)
+//       W_i  = K_i J_{i-1}^T ,  M_i = R + J_{i-1} W_i ,  L_i = W_i M_i^-1
+//       mu_i = u_i + W_i M_i^-1 (y_{i,i-1} - J_{i-1} u_i) ,  u_i = K_i g_i
+//       X_i  = P_i^-1 J_{i+1}^T , S_i = R - J_{i+1} X_i , G_i = X_i S_i^-1
+//  * waves 1-7 = HELPERS (448 lanes), one step behind / ahead of the solver:
+//       HB  next base K_i = B_i + rank-4, fused with node i-1's covariance
+//           P_{i-1}^-1 = B_i - L_{i-1} W_{i-1}^T, damped and stored (hw 0-5);
+//       HE  h_obs GEMV of node i+2 over the slice's (U,V): register-resident
+//           (node j -> helper lane j % 448, slot j / 448), overflow in LDS;
+//       HF1 AR(1) terms + natural parameter g_{i+1} (hw 0-2);
+//       HF2 v_{i+1} = K_i g_{i+1}, yv_{i+1} = K_i J_{i+2}^T (hw 3-6);
+//       HX  the 20 dot products of the step that do not involve mu_{i-1} (hw 3);
+//       LOADER (hw 6): LDS-DMA (global_load_lds) rings, 3 steps ahead, for Y
+//           rows, old covariances, old means and the hand-off granules, so no
+//           wave holds prefetch registers.
+//  * one workgroup barrier per step; intra-step hand-offs through LDS
+//    counters.
+#include "ame_common.h"
+#include "ame_wave.h"
+
+using namespace ame;
+
+#ifdef AME_STAMPS
+// Diagnostic build only (cdna_hip_programming.md §7, in-kernel stamps): the
+// middle lane records s_memtime at marked points of steps [S3_I0, S3_I0+16) for
+// waves 0 (solver), 1 (hw 0), 4 (hw 3) and 7 (hw 6); every lane records
+// s_memrealtime when it reaches steps 0, n/4, n/2, 3n/4 and n.
+#define S3_I0 256
+__device__ unsigned long long g_s3_stamps[4 * 16 * 16];
+__device__ unsigned long long g_s3_prog[256 * 5];
+#define S3W(w) ((w) == 0 ? 0 : (w) == 1 ? 1 : (w) == 4 ? 2 : (w) == 7 ? 3 : -1)
+#define STAMP3(slot)                                                                           \
+    do {                                                                                       \
+        if (tl == TL / 2 && lane == 0 && i >= S3_I0 && i < S3_I0 + 16 && S3W(wave) >= 0) {     \
+            unsigned long long t_;                                                             \
+            __builtin_amdgcn_sched_barrier(0);                                                 \
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");        \
+            __builtin_amdgcn_sched_barrier(0);                                                 \
+            g_s3_stamps[(S3W(wave) * 16 + (i - S3_I0)) * 16 + (slot)] = t_;                    \
+        }                                                                                      \
+    } while (0)
+#define PROG3()                                                                                \
+    do {                                                                                       \
+        if (tid == 0 && (i == 0 || i == n / 4 || i == n / 2 || i == 3 * n / 4 || i == n)) {    \
+            const int q_ = (i == 0) ? 0 : (i == n / 4) ? 1 : (i == n / 2) ? 2 : (i == 3 * n / 4) ? 3 : 4; \
+            g_s3_prog[tl * 5 + q_] = __builtin_amdgcn_s_memrealtime();                         \
+        }                                                                                      \
+    } while (0)
+extern "C" int ame_debug_read_stamps3(unsigned long long* st, unsigned long long* prog) {
+    if (hipMemcpyFromSymbol(st, HIP_SYMBOL(g_s3_stamps), sizeof(g_s3_stamps), 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    return hipMemcpyFromSymbol(prog, HIP_SYMBOL(g_s3_prog), sizeof(g_s3_prog), 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#else
+#define STAMP3(slot) do { } while (0)
+#define PROG3() do { } while (0)
+#endif
+
+namespace {
+
+constexpr int kNT = 512;    // threads per workgroup
+constexpr int kNH = 448;    // helper lanes
+constexpr int kMREG = 96;   // VGPR budget for the register-resident part of the node slice
+constexpr int kLDSMAX = 160 * 1024;
+
+template <int R>
+struct Cfg {
+    static constexpr int D = 2 + 2 * R, M2 = 2 * R, DD = D * D;
+    // node j -> helper lane j % 448, slot j / 448; slots < NSREG in registers,
+    // further slots in LDS ([slot][c/2][lane] float2: conflict-free reads)
+    static constexpr int NSREG = (kMREG / M2) < 1 ? 1 : ((kMREG / M2) > 16 ? 16 : (kMREG / M2));
+    static constexpr int MP = (M2 + 1) / 2;
+    static constexpr int NLT = D * (D + 1) / 2;
+    static constexpr int NHB = 384;                           // HB lanes (hw 0-5)
+    static constexpr int LTQ = (NLT + NHB - 1) / NHB;
+    static constexpr int NP = (4 * D <= 192) ? 4 : 2;       // AR row parts (HF1)
+    static constexpr int MC = (D + NP - 1) / NP;
+    static constexpr int NHALF = (6 * D <= 256) ? 2 : 1;    // HF2 row halves
+    static constexpr int HD = D / NHALF;
+    static constexpr int NC = (DD * 4 + 1023) / 1024;       // DMA KiB per covariance
+};
+
+// LDS carve-up (bytes); host and device agree.  Everything but the Y ring and
+// the overflow node slots has a compile-time offset (folds into ds_* immediate
+// offsets instead of occupying SGPRs).  Ring slots are whole KiB multiples: one
+// LDS-DMA instruction writes 64 lanes x 16 B = 1 KiB.
+__host__ __device__ constexpr int al16(int x) { return (x + 15) & ~15; }
+template <int R>
+struct Lay {
+    static constexpr int D = 2 + 2 * R, DD = D * D;
+    static constexpr int cs = ((DD * 4 + 1023) / 1024) * 256;     // covariance ring slot (floats)
+    static constexpr int oK = 0;                                   // base inverse, double buffer
+    static constexpr int oAR = al16(oK + 8 * 2 * DD);              // Qinv Phi, Phi^T Qinv (fp64)
+    static constexpr int oRec = al16(oAR + 8 * 2 * DD);            // [par][k]{L0 L1 W0 W1 G0 G1 X0 X1}
+    static constexpr int oMu64 = al16(oRec + 8 * 2 * D * 8);       // [par][k] new mean (fp64)
+    static constexpr int oMu32 = al16(oMu64 + 8 * 2 * D);          // [par][k] new mean (fp32)
+    static constexpr int oG = al16(oMu32 + 4 * 2 * D);             // [node&1][k] g of node
+    static constexpr int oJn = al16(oG + 8 * 2 * D);               // [q][k] J rows of node i+2 (old)
+    static constexpr int oV = al16(oJn + 8 * 2 * D);               // [node&1][k]{v, yv0, yv1, vA}
+    static constexpr int oDots = al16(oV + 8 * 2 * D * 4);         // HX results
+    static constexpr int oRed = al16(oDots + 8 * 32);              // solver reduction gather
+    static constexpr int oGP = al16(oRed + 8 * 64);                // [node&1][wave][k] GEMV partials
+    static constexpr int oYst = al16(oGP + 4 * 2 * 7 * D);         // [node&3]{y(m,m-1), y(m,m-2)} raw
+    static constexpr int oMuL = al16(oYst + 4 * 4 * 4);            // [wave][k] mu_{m,t-1}
+    static constexpr int oPd = al16(oMuL + 4 * 3 * D);             // [par][k] naive diag(P)
+    static constexpr int oFlag = al16(oPd + 8 * 2 * D);            // kcnt, ddone, gcnt
+    static constexpr int oCr = al16(oFlag + 16);                   // [node&3] old covariances, DMA
+    static constexpr int oXr = al16(oCr + 4 * 4 * cs);             // [node&7] old means slice t, DMA
+    static constexpr int oRr = al16(oXr + 8 * 256);                // [node&3] old means slice t+1, DMA
+    static constexpr int oPr = al16(oRr + 4 * 256);                // [node&3] hand-off granules, DMA
+    static constexpr int oYr = al16(oPr + 4 * 1024);               // [node&3] Y rows (raw), DMA
+    __host__ __device__ static int ys(int n) { return ((n * 8 + 1023) / 1024) * 128; }   // float2
+    __host__ __device__ static int oML(int n) { return al16(oYr + 4 * 8 * ys(n)); }
+    __host__ __device__ static int total(int n, int nsreg) {
+        const int nsl = (n + 447) / 448 - nsreg;
+        return al16(oML(n) + 8 * (nsl > 0 ? nsl : 0) * ((2 * R + 1) / 2) * 448);
+    }
+};
+
+__device__ __forceinline__ void lds_barrier3() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void wave_lds_sync3() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
+// LDS counters (workgroup-coherent); writers drain their LDS stores first.
+__device__ __forceinline__ void lds_signal_add(uint32_t* f, uint32_t v) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_signal_set(uint32_t* f, uint32_t v) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Bounded: a wait that outlives AME_SPIN_TICKS_LOCAL sets AME_STATUS_LDS_TIMEOUT
+// and gives up (the launch then finishes with wrong values, never hangs).
+__device__ __forceinline__ void lds_wait_ge(uint32_t* f, uint32_t target, uint32_t* status, bool& dead) {
+    if (!dead && __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > AME_SPIN_TICKS_LOCAL) {
+                if ((threadIdx.x & 63) == 0) atomicOr(status, AME_STATUS_LDS_TIMEOUT);
+                dead = true;
+                break;
+            }
+        }
+    }
+    asm volatile("" ::: "memory");
+}
+
+// LDS-DMA: each lane's 16 (4) bytes from gsrc land at LDS byte lds + lane*16 (*4).
+// Issued as inline asm so hipcc's waitcnt pass does not serialise LDS reads
+// behind it; the loader wave counts completion itself (vmcnt).
+__device__ __forceinline__ uint32_t lds_off(const void* p) {
+    return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)p);
+}
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void dma16_sc1(const void* gsrc, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc1\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void dma16_sys(const void* gsrc, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc0 sc1\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void dma4(const void* gsrc, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
+}
+// s_waitcnt vmcnt(<= n): waits for at most 3 more operations than asked.
+__device__ __forceinline__ void vm_wait_le(int n) {
+    if (n >= 60) asm volatile("s_waitcnt vmcnt(60)" ::: "memory");
+    else if (n >= 48) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+    else if (n >= 40) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+    else if (n >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    else if (n >= 28) asm volatile("s_waitcnt vmcnt(28)" ::: "memory");
+    else if (n >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else if (n >= 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+    else if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__device__ __forceinline__ void tri_decode3(int e, int& k, int& m) {
+    k = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+    if ((k + 1) * (k + 2) / 2 <= e) ++k;
+    if (k * (k + 1) / 2 > e) --k;
+    m = e - k * (k + 1) / 2;
+}
+
+// J entries of a node for state index k, from its (fp32) mean in LDS:
+// J = [[1, 0, V, 0], [0, 1, 0, U]]; zero when the node does not exist.
+template <int R>
+__device__ __forceinline__ void jcol(const float* mu, bool exists, int k, double& j0, double& j1) {
+    j0 = 0.0;
+    j1 = 0.0;
+    if (!exists) return;
+    if (k == 0) j0 = 1.0;
+    else if (k == 1) j1 = 1.0;
+    else if (k < 2 + R) j0 = (double)mu[2 + R + (k - 2)];
+    else j1 = (double)mu[2 + (k - 2 - R)];
+}
+
+__device__ __forceinline__ double dpp_add_xor1(double v) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = dpp_partner<5>((uint32_t)b), hi = dpp_partner<5>((uint32_t)(b >> 32));
+    return v + __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ __forceinline__ double dpp_add_mirror4(double v) {   // lane 0<->3, 1<->2
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = dpp_partner<4>((uint32_t)b), hi = dpp_partner<4>((uint32_t)(b >> 32));
+    return v + __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+}  // namespace
+
+template <int R>
+__global__ void __launch_bounds__(kNT)
+ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
+    using C = Cfg<R>;
+    constexpr int D = C::D, M2 = C::M2, DD = C::DD, NSREG = C::NSREG, MP = C::MP;
+    constexpr int NLT = C::NLT, LTQ = C::LTQ, NP = C::NP, MC = C::MC, NHALF = C::NHALF, HD = C::HD;
+    constexpr int NC = C::NC;
+    const int n = dm.n, TL = dm.T_local, Tt = dm.T_total;
+    const int b = blockIdx.x;
+    // XCD-aware lane order: consecutive time slices share an XCD (speed only)
+    const int tl = (TL % 8 == 0) ? ((b & 7) * (TL >> 3) + (b >> 3)) : b;
+    const int tg = dm.t_begin + tl;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int hl = tid - 64, hw = wave - 1;   // helper lane / helper wave (valid for wave >= 1)
+    const bool is_naive = dm.variant == AME_NAIVE, is_bad = dm.variant == AME_BAD;
+    const int ns = (n + kNH - 1) / kNH;
+    const int NY = (n * 8 + 1023) / 1024;     // DMA KiB per Y row
+    const int KDMA = NY + NC + 3;             // DMA instructions per step (loader wave)
+
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    using LY = Lay<R>;
+    const int YS = LY::ys(n);
+    double* Kbuf = (double*)(smem + LY::oK);
+    double* arQ = (double*)(smem + LY::oAR);          // Qinv Phi
+    double* arP = arQ + DD;                            // Phi^T Qinv
+    double* rec = (double*)(smem + LY::oRec);
+    double* mu64 = (double*)(smem + LY::oMu64);
+    float* mu32 = (float*)(smem + LY::oMu32);
+    double* g64 = (double*)(smem + LY::oG);
+    double* jn64 = (double*)(smem + LY::oJn);
+    double* vbuf = (double*)(smem + LY::oV);
+    double* dots = (double*)(smem + LY::oDots);
+    double* red = (double*)(smem + LY::oRed);
+    float* gp = (float*)(smem + LY::oGP);
+    float* yst = (float*)(smem + LY::oYst);
+    float* muL = (float*)(smem + LY::oMuL);
+    double* pdl = (double*)(smem + LY::oPd);
+    uint32_t* flags = (uint32_t*)(smem + LY::oFlag);
+    uint32_t* kcnt = flags;
+    uint32_t* ddone = flags + 1;
+    uint32_t* gcnt = flags + 2;
+    float2* yring = (float2*)(smem + LY::oYr);
+    float* cring = (float*)(smem + LY::oCr);
+    float* xring = (float*)(smem + LY::oXr);
+    float* rring = (float*)(smem + LY::oRr);
+    uint64_t* pring = (uint64_t*)(smem + LY::oPr);
+    float2* mlds = (float2*)(smem + LY::oML(n));
+
+    const double r00 = a.rinv[0], r01 = a.rinv[1], r10 = a.rinv[2], r11 = a.rinv[3];
+    const float r00f = (float)r00, r01f = (float)r01, r10f = (float)r10, r11f = (float)r11;
+    const Mat2 Rm = inv2s(m2(r00, r01, r10, r11));   // R = R_inv^-1, symmetrised
+    const float lr = a.lr, om = a.one_minus_lr;
+    const float* xo = a.x_old + (size_t)tl * n * D;
+    float* xn = a.x_new + (size_t)tl * n * D;
+    float* cvs = a.cov + (size_t)tl * n * DD;
+    const float* ysl = a.Yt + (size_t)tl * n * n * 2;
+    const float* xr = (tg < Tt - 1) ? ((tl < TL - 1) ? a.x_old + (size_t)(tl + 1) * n * D : a.next_old)
+                                    : nullptr;
+    const double* K0 = a.work + (size_t)tl * DD;
+    const double* ssq0 = a.work + (size_t)TL * DD + (size_t)tl * M2;
+    const double* QiPhi = a.consts + 3 * (size_t)DD;
+    bool dead = false;
+
+    // ---- hand-off of mu_{node, t-1} ----
+    auto gran_src = [&](int node) -> const uint64_t* {
+        return (tl == 0) ? a.halo_in + (size_t)node * D : a.hand + ((size_t)(tl - 1) * n + node) * D;
+    };
+    // v = granule of this lane (k = lane < D) as read earlier; spin until its tag is current
+    auto gran_finish = [&](int node, uint64_t v, float* dst) {
+        if (tg == 0) {
+            if (lane < D) dst[lane] = 0.f;
+            return;
+        }
+        bool ok = (lane >= D) || (uint32_t)(v >> 32) == a.epoch;
+        if (!__all(ok) && !dead) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            const uint64_t budget = (tl == 0) ? AME_SPIN_TICKS_HALO : AME_SPIN_TICKS_LOCAL;
+            const uint64_t* src = gran_src(node);
+            while (true) {
+                if (lane < D) {
+                    v = (tl == 0) ? gran_load_system(src + lane) : gran_load_agent(src + lane);
+                    ok = (uint32_t)(v >> 32) == a.epoch;
+                }
+                if (__all(ok)) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > budget) {
+                    if (lane == 0)
+                        atomicOr(a.status, (tl == 0) ? AME_STATUS_HALO_TIMEOUT : AME_STATUS_SPIN_TIMEOUT);
+                    dead = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        if (lane < D) dst[lane] = __uint_as_float((uint32_t)v);
+    };
+
+    // ---- loader DMA pieces (whole-wave; every call issues a fixed instruction count) ----
+    auto dma_y = [&](int row) {   // Y row (raw float2) -> slot row & 3 : NY instructions
+        const int rw = (row < n) ? row : 0;
+        const char* base = (const char*)(ysl + (size_t)rw * n * 2);
+        const uint32_t dst = lds_off(yring + (size_t)(row & 3) * YS);
+        for (int q = 0; q < NY; ++q) {
+            int off = (q * 64 + lane) * 16;
+            if (off >= n * 8) off = 0;
+            dma16(base + off, dst + q * 1024);
+        }
+    };
+    auto dma_cov = [&](int node) {   // old covariance -> slot node & 3 : NC instructions
+        const int cn = (node >= 0 && node < n) ? node : 0;
+        const char* base = (const char*)(cvs + (size_t)cn * DD);
+        const uint32_t dst = lds_off(cring + (size_t)(node & 3) * LY::cs);
+#pragma unroll
+        for (int q = 0; q < NC; ++q) {
+            int off = (q * 64 + lane) * 16;
+            if (off >= DD * 4) off = 0;
+            dma16(base + off, dst + q * 1024);
+        }
+    };
+    auto dma_x = [&](int node) {   // old mean, slice t -> slot node & 7 : 1 instruction
+        const int xnn = (node < n) ? node : 0;
+        dma4(xo + (size_t)xnn * D + (lane < D ? lane : 0), lds_off(xring + (node & 7) * 64));
+    };
+    auto dma_r = [&](int node) {   // old mean, slice t+1 -> slot node & 3 : 1 instruction
+        const float* src = (xr != nullptr && node < n) ? xr + (size_t)node * D : xo;
+        dma4(src + (lane < D ? lane : 0), lds_off(rring + (node & 3) * 64));
+    };
+    auto dma_p = [&](int node) {   // granules of mu_{node, t-1} -> slot node & 3 : 1 instruction
+        const uint32_t dst = lds_off(pring + (size_t)(node & 3) * 128);
+        const int g2 = (lane * 2 < D) ? lane * 2 : 0;
+        if (tg == 0 || node >= n) dma16(xo, dst);
+        else if (tl == 0) dma16_sys(gran_src(node) + g2, dst);
+        else dma16_sc1(gran_src(node) + g2, dst);
+    };
+
+    // ============================ prologue ============================
+    for (int e = tid; e < DD; e += kNT) Kbuf[e] = K0[e];
+    for (int e = tid; e < 2 * DD; e += kNT) arQ[e] = QiPhi[e];   // QiPhi, PhiTQi are adjacent
+    for (int e = tid; e < 2 * D * 8; e += kNT) rec[e] = 0.0;
+    for (int e = tid; e < 2 * D; e += kNT) {
+        mu64[e] = 0.0;
+        mu32[e] = 0.f;
+    }
+    if (tid < 16) yst[tid] = 0.f;
+    if (tid < 4) flags[tid] = 0u;
+    float mreg[NSREG][M2];      // (U, V) of nodes hl + 448 s, s < NSREG
+    if (wave >= 1) {
+#pragma unroll
+        for (int s = 0; s < NSREG; ++s) {
+            const int j = hl + kNH * s;
+            const bool ok = s < ns && j < n;
+#pragma unroll
+            for (int c = 0; c < M2; ++c) mreg[s][c] = ok ? xo[(size_t)j * D + 2 + c] : 0.f;
+        }
+        for (int s = NSREG; s < ns; ++s) {
+            const int j = hl + kNH * s;
+            const bool ok = j < n;
+            for (int c2 = 0; c2 < MP; ++c2) {
+                float2 v = make_float2(0.f, 0.f);
+                if (ok) {
+                    v.x = xo[(size_t)j * D + 2 + 2 * c2];
+                    if (2 * c2 + 1 < M2) v.y = xo[(size_t)j * D + 3 + 2 * c2];
+                }
+                mlds[((s - NSREG) * MP + c2) * kNH + hl] = v;
+            }
+        }
+        // Y rows 0 and 1 into ring slots 0 and 1 (plain loads)
+        for (int e = hl; e < 2 * n; e += kNH) {
+            const int rw = e / n, j = e - rw * n;
+            yring[(size_t)rw * YS + j] = (rw < n) ? *(const float2*)(ysl + ((size_t)rw * n + j) * 2)
+                                                    : make_float2(0.f, 0.f);
+        }
+    }
+    double ssq_l = 0.0;   // solver, naive: running sum of squares of column `lane`
+    if (tid < D && is_naive && tid >= 2) ssq_l = ssq0[tid - 2];
+    if (wave == 7) {   // rings read by steps 0..2 and the prologue
+        for (int q = 0; q < 5; ++q) dma_x(q);
+        for (int q = 0; q < 4; ++q) dma_r(q);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+
+    // GEMV of node m over nodes j (excluding j in {m-2, m-1, m}) from raw Y values
+    // ysrc[j]; stashes y_{m,m-1}, y_{m,m-2}; partials -> gp[m&1][hw][.]
+    auto gemv = [&](int m, const float2* ysrc) {
+        float acc[D];
+#pragma unroll
+        for (int c = 0; c < D; ++c) acc[c] = 0.f;
+#pragma unroll
+        for (int s = 0; s < NSREG; ++s) {
+            if (s < ns) {
+                const int j = hl + kNH * s;
+                const float2 y = (j < n) ? ysrc[j] : make_float2(0.f, 0.f);
+                if (j == m - 1) { yst[(m & 3) * 4 + 0] = y.x; yst[(m & 3) * 4 + 1] = y.y; }
+                if (j == m - 2) { yst[(m & 3) * 4 + 2] = y.x; yst[(m & 3) * 4 + 3] = y.y; }
+                float z0 = r00f * y.x + r01f * y.y;
+                float z1 = r10f * y.x + r11f * y.y;
+                if (j >= m - 2 && j <= m) { z0 = 0.f; z1 = 0.f; }
+                acc[0] += z0;
+                acc[1] += z1;
+#pragma unroll
+                for (int c = 0; c < R; ++c) {
+                    acc[2 + c] = fmaf(z0, mreg[s][R + c], acc[2 + c]);       // h_U += z0 V
+                    acc[2 + R + c] = fmaf(z1, mreg[s][c], acc[2 + R + c]);   // h_V += z1 U
+                }
+            }
+        }
+        for (int s = NSREG; s < ns; ++s) {
+            const int j = hl + kNH * s;
+            const float2 y = (j < n) ? ysrc[j] : make_float2(0.f, 0.f);
+            if (j == m - 1) { yst[(m & 3) * 4 + 0] = y.x; yst[(m & 3) * 4 + 1] = y.y; }
+            if (j == m - 2) { yst[(m & 3) * 4 + 2] = y.x; yst[(m & 3) * 4 + 3] = y.y; }
+            float z0 = r00f * y.x + r01f * y.y;
+            float z1 = r10f * y.x + r11f * y.y;
+            if (j >= m - 2 && j <= m) { z0 = 0.f; z1 = 0.f; }
+            acc[0] += z0;
+            acc[1] += z1;
+            const float2* ml = mlds + (size_t)(s - NSREG) * MP * kNH + hl;
+#pragma unroll
+            for (int c2 = 0; c2 < MP; ++c2) {   // column c: U_c -> h_V (z1), V_c -> h_U (z0)
+                const float2 t = ml[c2 * kNH];
+                const int c = 2 * c2;
+                if (c < R) acc[2 + R + c] = fmaf(z1, t.x, acc[2 + R + c]);
+                else acc[2 + (c - R)] = fmaf(z0, t.x, acc[2 + (c - R)]);
+                if (c + 1 < M2) {
+                    if (c + 1 < R) acc[2 + R + c + 1] = fmaf(z1, t.y, acc[2 + R + c + 1]);
+                    else acc[2 + (c + 1 - R)] = fmaf(z0, t.y, acc[2 + (c + 1 - R)]);
+                }
+                if ((c2 & 3) == 3) asm volatile("" ::: "memory");
+            }
+        }
+        int idx;
+        const float v = wave_reduce_scatter<D>(acc, lane, idx);
+        if (idx < D) gp[((m & 1) * 7 + hw) * D + idx] = v;
+    };
+    // HF1 (hw 0..2): AR terms + natural parameter g of node m.
+    // mu_{m,t-1} in muL[hw], mu_{m,t+1}^old in rring[m&3].
+    auto hf1 = [&](int m) {
+        const int q = hl;   // 0..191
+        const int k = q / NP, p = q - k * NP;
+        double acc = 0.0;
+        if (k < D) {
+            const float* ml = muL + hw * D;
+            const float* mr = rring + (m & 3) * 64;
+#pragma unroll
+            for (int mm = 0; mm < MC; ++mm) {
+                const int c = p * MC + mm;
+                if (c < D) {
+                    if (tg > 0) acc = fma(arQ[k * D + c], (double)ml[c], acc);
+                    if (tg < Tt - 1) acc = fma(arP[k * D + c], (double)mr[c], acc);
+                }
+            }
+        }
+        acc = dpp_add_xor1(acc);
+        if constexpr (NP == 4) acc = dpp_add_mirror4(acc);
+        if (k < D && p == 0) {
+            double g = 0.0;
+#pragma unroll
+            for (int w = 0; w < 7; ++w) g += (double)gp[((m & 1) * 7 + w) * D + k];
+            g += acc;
+            if (m >= 2) {   // node m-2 was excluded from the GEMV; its new mean is known now
+                const float* mup = mu32 + ((m - 2) & 1) * D;
+                double j0, j1;
+                jcol<R>(mup, true, k, j0, j1);
+                const double y0 = (double)yst[(m & 3) * 4 + 2], y1 = (double)yst[(m & 3) * 4 + 3];
+                const double z0 = r00 * y0 + r01 * y1, z1 = r10 * y0 + r11 * y1;
+                g = fma(j0, z0, fma(j1, z1, g));
+            }
+            g64[(m & 1) * D + k] = g;
+        }
+    };
+    // HF2 (hw 3..6): v = K g, yv = K Jn^T for node m with base Kb
+    auto hf2 = [&](int m, const double* Kb) {
+        const int q = tid - 256;
+        const int k = q / (3 * NHALF), rem = q - k * (3 * NHALF);
+        const int vsel = rem / NHALF, half = rem - vsel * NHALF;
+        double acc = 0.0, accA = 0.0;
+        if (k < D) {
+            const double* vec = (vsel == 0) ? g64 + (m & 1) * D : jn64 + (vsel - 1) * D;
+            const double* kr = Kb + (size_t)k * D;
+            const int c0 = half * HD;
+#pragma unroll
+            for (int c = 0; c < HD; ++c) {
+                acc = fma(kr[c0 + c], vec[c0 + c], acc);
+                if ((c & 3) == 3) asm volatile("" ::: "memory");
+            }
+            if (vsel == 0 && half == 0) accA = kr[0] * vec[0] + kr[1] * vec[1];
+        }
+        if constexpr (NHALF == 2) acc = dpp_add_xor1(acc);
+        if (k < D && half == 0) {
+            double* vo = vbuf + ((m & 1) * D + k) * 4;
+            vo[vsel] = acc;
+            if (vsel == 0) vo[3] = accA;
+        }
+    };
+    auto jn_fill = [&](int node) {   // J rows of `node` (old) -> jn64; lanes < D of the calling wave
+        if (lane < D) {
+            double j0, j1;
+            jcol<R>(xring + (node & 7) * 64, node < n, lane, j0, j1);
+            jn64[lane] = j0;
+            jn64[D + lane] = j1;
+        }
+    };
+
+    // ---- prologue work: g_0, GEMV partials of node 1, v_0 / yv_0; rings for steps 0..2 ----
+    if (wave >= 1) {
+        gemv(0, yring);
+        gemv(1, yring + YS);
+        if (hw <= 2) {
+            uint64_t g0 = 0;
+            if (tg > 0 && lane < D)
+                g0 = (tl == 0) ? gran_load_system(gran_src(0) + lane) : gran_load_agent(gran_src(0) + lane);
+            gran_finish(0, g0, muL + hw * D);
+        }
+        if (hw == 3) jn_fill(1);
+    }
+    __syncthreads();
+    if (wave >= 1 && hw <= 2) hf1(0);
+    __syncthreads();
+    if (wave >= 4) hf2(0, Kbuf);
+    if (wave == 7) {   // Y rows 2..4 (slots 2,3,0), covariances of nodes 0,1, granules of nodes 1..3
+        for (int q = 2; q <= 4; ++q) dma_y(q);
+        for (int q = 0; q <= 1; ++q) dma_cov(q);
+        for (int q = 1; q <= 3; ++q) dma_p(q);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+
+    if (wave == 0) {
+        // ============================ SOLVER ============================
+        __builtin_amdgcn_s_setprio(3);
+        const int k = lane;
+        const bool kl = k < D;
+        double brow[D];   // row k of the base inverse B_i
+#pragma unroll
+        for (int c = 0; c < D; ++c) brow[c] = kl ? Kbuf[(size_t)k * D + c] : 0.0;
+        double Wp0 = 0, Wp1 = 0, Xp0 = 0, Xp1 = 0, Lp0 = 0, Lp1 = 0, Gp0 = 0, Gp1 = 0;
+        Mat2 Mip = m2(0, 0, 0, 0), Sip = m2(0, 0, 0, 0);
+        for (int i = 0; i < n; ++i) {
+            PROG3();
+            STAMP3(0);
+            const int par = i & 1, ppar = (i + 1) & 1;
+            const bool has_prev = i > 0;
+            const float* mup = mu32 + ppar * D;       // mu_{i-1} (fp32)
+            const double* mupd = mu64 + ppar * D;     // mu_{i-1} (fp64)
+            double v = 0, yv0 = 0, yv1 = 0, vA = 0, g = 0;
+            if (kl) {
+                const double* vi = vbuf + (par * D + k) * 4;
+                v = vi[0]; yv0 = vi[1]; yv1 = vi[2]; vA = vi[3];
+                g = g64[par * D + k];
+            }
+            double J0 = 0, J1 = 0;
+            if (kl) jcol<R>(mup, has_prev, k, J0, J1);
+            // kj = B J^T (the one critical matvec)
+            double kj0 = 0, kj1 = 0;
+            if (has_prev) {
+                double s0a = brow[0], s0b = 0, s1a = brow[1], s1b = 0;
+#pragma unroll
+                for (int c = 0; c < R; c += 2) {
+                    s0a = fma(brow[2 + c], mupd[2 + R + c], s0a);
+                    s1a = fma(brow[2 + R + c], mupd[2 + c], s1a);
+                    if (c + 1 < R) {
+                        s0b = fma(brow[3 + c], mupd[3 + R + c], s0b);
+                        s1b = fma(brow[3 + R + c], mupd[3 + c], s1b);
+                    }
+                }
+                kj0 = s0a + s0b;
+                kj1 = s1a + s1b;
+            }
+            STAMP3(1);
+            // critical reduction: a1(4) a2(4) c(4) e(2) jy(4) eA(2)
+            constexpr int NV = 20;
+            double pr[NV];
+            pr[0] = Wp0 * J0; pr[1] = Wp0 * J1; pr[2] = Wp1 * J0; pr[3] = Wp1 * J1;       // a1[p][q]
+            pr[4] = Xp0 * J0; pr[5] = Xp0 * J1; pr[6] = Xp1 * J0; pr[7] = Xp1 * J1;       // a2[p][q]
+            pr[8] = J0 * kj0; pr[9] = J0 * kj1; pr[10] = J1 * kj0; pr[11] = J1 * kj1;     // c[q][p]
+            pr[12] = J0 * v; pr[13] = J1 * v;                                             // e[q]
+            pr[14] = J0 * yv0; pr[15] = J0 * yv1; pr[16] = J1 * yv0; pr[17] = J1 * yv1;   // jy[q][p]
+            pr[18] = J0 * vA; pr[19] = J1 * vA;                                           // eA[q]
+            {
+                int idx;
+                const double sv = wave_reduce_scatter<NV>(pr, lane, idx);
+                if (idx < NV) red[idx] = sv;
+            }
+            wave_lds_sync3();
+            double o[NV];
+#pragma unroll
+            for (int q = 0; q < NV; ++q) o[q] = red[q];
+            const Mat2 a1 = m2(o[0], o[1], o[2], o[3]);
+            const Mat2 a2 = m2(o[4], o[5], o[6], o[7]);
+            const Mat2 cc = m2(o[8], o[9], o[10], o[11]);
+            const V2 e = {o[12], o[13]};
+            const Mat2 jy = m2(o[14], o[15], o[16], o[17]);
+            const V2 eA = {o[18], o[19]};
+            STAMP3(2);
+            // off-critical dots from helper wave hw 3
+            lds_wait_ge(ddone, (uint32_t)(i + 1), a.status, dead);
+            STAMP3(3);
+            const V2 b1 = {dots[0], dots[1]}, b2 = {dots[2], dots[3]};
+            const Mat2 f1 = m2(dots[4], dots[5], dots[6], dots[7]);
+            const Mat2 f2 = m2(dots[8], dots[9], dots[10], dots[11]);
+            const Mat2 ny = m2(dots[12], dots[13], dots[14], dots[15]);
+            const V2 b1A = {dots[16], dots[17]}, b2A = {dots[18], dots[19]};
+            // raw y_{i,i-1}
+            double y0 = 0, y1 = 0;
+            if (has_prev) { y0 = (double)yst[(i & 3) * 4 + 0]; y1 = (double)yst[(i & 3) * 4 + 1]; }
+            const double zp0 = r00 * y0 + r01 * y1, zp1 = r10 * y0 + r11 * y1;
+            // ---- 2x2 algebra ----
+            const Mat2 JW = add(sub(cc, quad(a1, Mip, a1)), quad(a2, Sip, a2));
+            const Mat2 Mm = add(Rm, sym(JW));
+            const Mat2 Mi = has_prev ? inv2s(Mm) : m2(0, 0, 0, 0);
+            const V2 t1 = mtv(a1, mv(Mip, b1)), t2 = mtv(a2, mv(Sip, b2));
+            const V2 Ju = {e.x - t1.x + t2.x, e.y - t1.y + t2.y};
+            const V2 cvec = mv(Mi, V2{y0 - Ju.x, y1 - Ju.y});
+            const Mat2 wn = add(sub(jy, quad(a1, Mip, f1)), quad(a2, Sip, f2));
+            const Mat2 JnK = add(sub(ny, quad(f1, Mip, f1)), quad(f2, Sip, f2));
+            const Mat2 JnX = sub(JnK, quad(wn, Mi, wn));
+            const Mat2 Si = inv2s(sub(Rm, sym(JnX)));
+            // ---- lane-local assembly ----
+            const double W0 = kj0 - (Lp0 * a1.a + Lp1 * a1.c) + (Gp0 * a2.a + Gp1 * a2.c);
+            const double W1 = kj1 - (Lp0 * a1.b + Lp1 * a1.d) + (Gp0 * a2.b + Gp1 * a2.d);
+            const double u = v - (Lp0 * b1.x + Lp1 * b1.y) + (Gp0 * b2.x + Gp1 * b2.y);
+            const double kn0 = yv0 - (Lp0 * f1.a + Lp1 * f1.c) + (Gp0 * f2.a + Gp1 * f2.c);
+            const double kn1 = yv1 - (Lp0 * f1.b + Lp1 * f1.d) + (Gp0 * f2.b + Gp1 * f2.d);
+            double mus;
+            if (!is_bad) {
+                mus = u + W0 * cvec.x + W1 * cvec.y;
+            } else {
+                const double uA = vA - (Lp0 * b1A.x + Lp1 * b1A.y) + (Gp0 * b2A.x + Gp1 * b2A.y);
+                const V2 s1 = mtv(a1, mv(Mip, b1A)), s2 = mtv(a2, mv(Sip, b2A));
+                const V2 JuA = {eA.x - s1.x + s2.x, eA.y - s1.y + s2.y};
+                // K_i[:, 0:2] (row k) and W_i rows 0, 1 (uniform)
+                const double* r0 = rec + (ppar * D + 0) * 8;
+                const double* r1 = rec + (ppar * D + 1) * 8;
+                const double KE0 = brow[0] - (Lp0 * r0[2] + Lp1 * r0[3]) + (Gp0 * r0[6] + Gp1 * r0[7]);
+                const double KE1 = brow[1] - (Lp0 * r1[2] + Lp1 * r1[3]) + (Gp0 * r1[6] + Gp1 * r1[7]);
+                const double WE00 = __shfl(W0, 0), WE01 = __shfl(W1, 0);   // W row 0
+                const double WE10 = __shfl(W0, 1), WE11 = __shfl(W1, 1);   // W row 1
+                const double wz0 = WE00 * zp0 + WE10 * zp1, wz1 = WE01 * zp0 + WE11 * zp1;
+                const double tA = uA + KE0 * zp0 + KE1 * zp1;
+                const V2 jA = {JuA.x + wz0, JuA.y + wz1};
+                const double tX = (u - uA) + (W0 * zp0 + W1 * zp1) - (KE0 * zp0 + KE1 * zp1);
+                const V2 jX = {(Ju.x - JuA.x) + (JW.a * zp0 + JW.b * zp1) - wz0,
+                               (Ju.y - JuA.y) + (JW.c * zp0 + JW.d * zp1) - wz1};
+                const V2 cA = mv(Mi, jA), cX = mv(Mi, jX);
+                mus = (k < 2) ? (tA - (W0 * cA.x + W1 * cA.y)) : (tX - (W0 * cX.x + W1 * cX.y));
+            }
+            if (!is_naive) mus += 1e-6 * (g + J0 * zp0 + J1 * zp1);
+            const double Ln0 = W0 * Mi.a + W1 * Mi.c, Ln1 = W0 * Mi.b + W1 * Mi.d;
+            const double Xn0 = kn0 - (Ln0 * wn.a + Ln1 * wn.c);
+            const double Xn1 = kn1 - (Ln0 * wn.b + Ln1 * wn.d);
+            const double Gn0 = Xn0 * Si.a + Xn1 * Si.c, Gn1 = Xn0 * Si.b + Xn1 * Si.d;
+            STAMP3(4);
+            // naive: diag(P_i) from running sums of squares (own old value removed)
+            double sq_other = 0.0;
+            if (is_naive) {
+                const int src = (k >= 2 && k < 2 + R) ? k + R : ((k >= 2 + R && k < D) ? k - R : k);
+                sq_other = __shfl(ssq_l, src);
+            }
+            // ---- publish ----
+            if (kl) {
+                const float* xold = xring + (i & 7) * 64;
+                const float mold = xold[k];
+                const float nw = __fadd_rn(__fmul_rn(lr, (float)mus), __fmul_rn(om, mold));
+                xn[(size_t)i * D + k] = nw;
+                const uint64_t gr = ((uint64_t)a.epoch << 32) | (uint64_t)__float_as_uint(nw);
+                gran_store_agent(a.hand + ((size_t)tl * n + i) * D + k, gr);
+                if (tl == TL - 1 && a.halo_out != nullptr)
+                    gran_store_system(a.halo_out + (size_t)i * D + k, gr);
+                mu32[par * D + k] = nw;
+                mu64[par * D + k] = (double)nw;
+                double* rc = rec + (par * D + k) * 8;
+                rc[0] = Ln0; rc[1] = Ln1; rc[2] = W0; rc[3] = W1;
+                rc[4] = Gn0; rc[5] = Gn1; rc[6] = Xn0; rc[7] = Xn1;
+                if (is_naive) {
+                    const double p = r00, s = r11;
+                    double pd;
+                    if (k == 0) pd = p * (double)(n - 1);
+                    else if (k == 1) pd = s * (double)(n - 1);
+                    else {
+                        const double oo = (k < 2 + R) ? (double)xold[k + R] : (double)xold[k - R];
+                        pd = ((k < 2 + R) ? p : s) * (sq_other - oo * oo);
+                    }
+                    pdl[par * D + k] = pd + pconst_entry(a.consts, D, k, k, tg, Tt);
+                    const double mo = (double)mold, mn = (double)nw;
+                    if (k >= 2) ssq_l = ssq_l - mo * mo + mn * mn;
+                }
+            }
+            Wp0 = W0; Wp1 = W1; Xp0 = Xn0; Xp1 = Xn1; Lp0 = Ln0; Lp1 = Ln1; Gp0 = Gn0; Gp1 = Gn1;
+            Mip = Mi;
+            Sip = Si;
+            STAMP3(5);
+            // next base rows, once every helper wave has written K_i
+            lds_wait_ge(kcnt, 7u * (uint32_t)(i + 1), a.status, dead);
+            STAMP3(6);
+            const double* Kn = Kbuf + (size_t)ppar * DD;
+            if (kl) {
+#pragma unroll
+                for (int c = 0; c < D; ++c) brow[c] = Kn[(size_t)k * D + c];
+            }
+            STAMP3(7);
+            lds_barrier3();
+        }
+        {
+            const int i = n;
+            PROG3();
+        }
+        lds_barrier3();   // epilogue step n
+    } else {
+        // ============================ HELPERS ============================
+        int lk[LTQ], lm[LTQ];
+#pragma unroll
+        for (int q = 0; q < LTQ; ++q) {
+            const int e = hl + C::NHB * q;
+            int k = -1, m = -1;
+            if (hl < C::NHB && e < NLT) tri_decode3(e, k, m);
+            lk[q] = k;
+            lm[q] = m;
+        }
+        for (int i = 0; i <= n; ++i) {
+            STAMP3(0);
+            const int par = i & 1, ppar = (i + 1) & 1;
+            const double* Bi = Kbuf + (size_t)par * DD;      // B_i
+            double* Kn = Kbuf + (size_t)ppar * DD;           // K_i = B_{i+1}
+            // HX (hw 3): dots that do not involve mu_{i-1}
+            if (hw == 3 && i < n) {
+                const int k = lane;
+                double pr[20];
+#pragma unroll
+                for (int q = 0; q < 20; ++q) pr[q] = 0.0;
+                if (k < D) {
+                    const double* rc = rec + (ppar * D + k) * 8;
+                    const double W0 = rc[2], W1 = rc[3], X0 = rc[6], X1 = rc[7];
+                    const double g = g64[par * D + k];
+                    const double yv0 = vbuf[(par * D + k) * 4 + 1], yv1 = vbuf[(par * D + k) * 4 + 2];
+                    double n0, n1;
+                    jcol<R>(xring + ((i + 1) & 7) * 64, i + 1 < n, k, n0, n1);
+                    const double gA = (k < 2) ? g : 0.0;
+                    pr[0] = W0 * g; pr[1] = W1 * g; pr[2] = X0 * g; pr[3] = X1 * g;           // b1, b2
+                    pr[4] = W0 * n0; pr[5] = W0 * n1; pr[6] = W1 * n0; pr[7] = W1 * n1;       // f1[p][q]
+                    pr[8] = X0 * n0; pr[9] = X0 * n1; pr[10] = X1 * n0; pr[11] = X1 * n1;     // f2[p][q]
+                    pr[12] = n0 * yv0; pr[13] = n0 * yv1; pr[14] = n1 * yv0; pr[15] = n1 * yv1; // ny[q][p]
+                    pr[16] = W0 * gA; pr[17] = W1 * gA; pr[18] = X0 * gA; pr[19] = X1 * gA;   // b1A, b2A
+                }
+                int idx;
+                const double sv = wave_reduce_scatter<20>(pr, lane, idx);
+                if (idx < 20) dots[idx] = sv;
+                if (lane == 0) lds_signal_set(ddone, (uint32_t)(i + 1));
+                STAMP3(1);
+            }
+            // HB (hw 0..5): K_i = B_i - L W^T + G X^T, fused covariance of node i-1
+            if (hw <= 5) {
+                const double* rp = rec + (size_t)ppar * D * 8;
+                const double* pdp = pdl + (size_t)ppar * D;
+                const float* co = cring + (size_t)((i + 3) & 3) * LY::cs;   // node i-1
+                float* cv = cvs + (size_t)(i > 0 ? i - 1 : 0) * DD;
+#pragma unroll
+                for (int q = 0; q < LTQ; ++q) {
+                    const int k = lk[q], m = lm[q];
+                    if (k < 0) continue;
+                    const double* rk = rp + k * 8;
+                    const double* rm = rp + m * 8;
+                    const double c = Bi[k * D + m] - (rk[0] * rm[2] + rk[1] * rm[3]);
+                    if (i < n) {
+                        const double kn = c + (rk[4] * rm[6] + rk[5] * rm[7]);
+                        Kn[k * D + m] = kn;
+                        Kn[m * D + k] = kn;
+                    }
+                    if (i >= 1) {
+                        float c32;
+                        if (is_naive) {
+                            c32 = (k == m) ? 1.0f / ((float)pdp[k] + 1e-8f) : 0.f;
+                        } else {
+                            c32 = (float)c;
+                            if (is_bad && ((k < 2) != (m < 2))) c32 = 0.f;
+                            if (k == m) c32 = c32 + 1e-6f;
+                        }
+                        cv[k * D + m] = __fadd_rn(__fmul_rn(lr, c32), __fmul_rn(om, co[k * D + m]));
+                        if (k != m) cv[m * D + k] = __fadd_rn(__fmul_rn(lr, c32), __fmul_rn(om, co[m * D + k]));
+                    }
+                }
+            }
+            STAMP3(4);
+            if (lane == 0) lds_signal_add(kcnt, 1u);
+            // HF1 (hw 0..2): hand-off of mu_{i+1,t-1} (DMA'd 3 steps ago), AR terms, g_{i+1}
+            if (hw <= 2 && i + 1 < n) {
+                uint64_t gv = 0;
+                if (lane < D) gv = pring[(size_t)((i + 1) & 3) * 128 + lane];
+                gran_finish(i + 1, gv, muL + hw * D);
+                STAMP3(2);
+                wave_lds_sync3();
+                hf1(i + 1);
+                STAMP3(3);
+                if (hw == 0) jn_fill(i + 2);   // J rows of node i+2 for HF2
+                if (lane == 0) lds_signal_add(gcnt, 1u);
+            }
+            if (i < n) {
+                // M update with mu_{i-1} (owner lane)
+                if (i >= 1) {
+                    const int j = i - 1, so = j / kNH, ho = j - so * kNH;
+                    if (hl == ho) {
+                        const float* mup = mu32 + ppar * D;
+                        if (so < NSREG) {
+#pragma unroll
+                            for (int s = 0; s < NSREG; ++s)
+                                if (s == so) {
+#pragma unroll
+                                    for (int c = 0; c < M2; ++c) mreg[s][c] = mup[2 + c];
+                                }
+                        } else {
+                            for (int c2 = 0; c2 < MP; ++c2) {
+                                float2 v = make_float2(mup[2 + 2 * c2], 0.f);
+                                if (2 * c2 + 1 < M2) v.y = mup[3 + 2 * c2];
+                                mlds[((so - NSREG) * MP + c2) * kNH + hl] = v;
+                            }
+                        }
+                    }
+                }
+                // HE: GEMV of node i+2 (its Y row landed in the ring by step i-1)
+                if (i + 2 < n) gemv(i + 2, yring + (size_t)((i + 2) & 3) * YS);
+                STAMP3(5);
+                // loader: this step's batch -- Y row i+5, covariance of node i+2, old
+                // means of node i+5 (slice t) and i+4 (slice t+1), granules of node i+4
+                if (hw == 6) {
+                    dma_y(i + 5);
+                    dma_cov(i + 2);
+                    dma_x(i + 5);
+                    dma_r(i + 4);
+                    dma_p(i + 4);
+                    STAMP3(6);
+                }
+                // HF2 (hw 3..6): v_{i+1}, yv_{i+1} with K_i
+                if (hw >= 3 && i + 1 < n) {
+                    lds_wait_ge(kcnt, 7u * (uint32_t)(i + 1), a.status, dead);
+                    lds_wait_ge(gcnt, 3u * (uint32_t)(i + 1), a.status, dead);
+                    STAMP3(7);
+                    hf2(i + 1, Kn);
+                    STAMP3(8);
+                }
+            }
+            // the batch issued 2 steps ago must have landed before the next step reads it
+            if (hw == 6) vm_wait_le(2 * KDMA);
+            STAMP3(9);
+            lds_barrier3();
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// prep: per slice P_0 = Pconst + sum_{j >= 1} F_j(old) in fp64, its inverse
+// K_0 (in-place symmetric sweep operator), and the naive variant's column sums
+// of squares.  One 256-thread workgroup per slice.
+// ---------------------------------------------------------------------------
+template <int R>
+__global__ void __launch_bounds__(AME_NT)
+ame_sweep3_prep_kernel(ame_dims dm, const float* __restrict__ x_old, const double* __restrict__ consts,
+                       double r00, double r01, double r10, double r11, double* __restrict__ work) {
+    constexpr int D = 2 + 2 * R, M2 = 2 * R, NLT = D * (D + 1) / 2, DD = D * D;
+    constexpr int CH = 64;   // nodes staged per chunk
+    const int n = dm.n, TL = dm.T_local, Tt = dm.T_total;
+    const int tl = blockIdx.x, tg = dm.t_begin + tl;
+    const int tid = threadIdx.x;
+    __shared__ float st[CH * M2];
+    __shared__ double K[DD];
+    __shared__ double piv[D];
+    const float* xs = x_old + (size_t)tl * n * D;
+    const double p = r00, s = r11, q = 0.5 * (r01 + r10);
+    constexpr int EQ = (NLT + AME_NT - 1) / AME_NT;
+    double acc[EQ];
+    int ek[EQ], em[EQ];
+#pragma unroll
+    for (int u = 0; u < EQ; ++u) {
+        acc[u] = 0.0;
+        const int e = tid + AME_NT * u;
+        int k = -1, m = -1;
+        if (e < NLT) tri_decode3(e, k, m);
+        ek[u] = k;
+        em[u] = m;
+    }
+    double sq = 0.0;   // thread tid < M2: sum over all nodes of column tid squared
+    for (int j0 = 1; j0 < n; j0 += CH) {   // nodes j >= 1
+        const int cnt = min(CH, n - j0);
+        __syncthreads();
+        for (int e = tid; e < cnt * M2; e += AME_NT) {
+            const int jj = e / M2, c = e - jj * M2;
+            st[e] = xs[(size_t)(j0 + jj) * D + 2 + c];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < EQ; ++u) {
+            const int k = ek[u], m = em[u];
+            if (k < 2) continue;
+            const int ck = k - 2;
+            const bool ku = ck < R;                      // row U_ck: J entry V ; row V: J entry U
+            const int kc = ku ? R + ck : ck - R;
+            if (m < 2) {
+                double a0 = 0.0;
+                for (int jj = 0; jj < cnt; ++jj) a0 += (double)st[jj * M2 + kc];
+                acc[u] += a0;
+            } else {
+                const int cm = m - 2;
+                const int mc = (cm < R) ? R + cm : cm - R;
+                double a0 = 0.0;
+                for (int jj = 0; jj < cnt; ++jj)
+                    a0 = fma((double)st[jj * M2 + kc], (double)st[jj * M2 + mc], a0);
+                acc[u] += a0;
+            }
+        }
+        if (tid < M2)
+            for (int jj = 0; jj < cnt; ++jj) {
+                const double v = (double)st[jj * M2 + tid];
+                sq = fma(v, v, sq);
+            }
+    }
+    if (tid < M2) {   // add node 0 to the sums of squares
+        const double v = (double)xs[2 + tid];
+        work[(size_t)TL * DD + (size_t)tl * M2 + tid] = fma(v, v, sq);
+    }
+#pragma unroll
+    for (int u = 0; u < EQ; ++u) {
+        const int k = ek[u], m = em[u];
+        if (k < 0) continue;
+        double v;
+        if (k < 2) {
+            v = ((k == 0 && m == 0) ? p : (k == 1 && m == 1) ? s : q) * (double)(n - 1);
+        } else {
+            const int ck = k - 2;
+            const bool ku = ck < R;
+            if (m < 2) {
+                v = (ku ? (m == 0 ? p : q) : (m == 0 ? q : s)) * acc[u];
+            } else {
+                const bool mu_ = (m - 2) < R;
+                v = ((ku && mu_) ? p : ((!ku && !mu_) ? s : q)) * acc[u];
+            }
+        }
+        v += pconst_entry(consts, D, k, m, tg, Tt);
+        K[k * D + m] = v;
+        K[m * D + k] = v;
+    }
+    __syncthreads();
+    for (int pv = 0; pv < D; ++pv) {   // in-place symmetric sweep: K -> -P_0^-1
+        if (tid < D) piv[tid] = K[pv * D + tid];
+        __syncthreads();
+        const double rinv = 1.0 / piv[pv];
+        for (int e = tid; e < NLT; e += AME_NT) {
+            int k, m;
+            tri_decode3(e, k, m);
+            double v;
+            if (k == pv && m == pv) v = -rinv;
+            else if (k == pv) v = piv[m] * rinv;
+            else if (m == pv) v = piv[k] * rinv;
+            else v = K[k * D + m] - (piv[k] * piv[m]) * rinv;
+            K[k * D + m] = v;
+            K[m * D + k] = v;
+        }
+        __syncthreads();
+    }
+    double* K0 = work + (size_t)tl * DD;
+    for (int e = tid; e < DD; e += AME_NT) K0[e] = -K[e];
+}
+
+
+template <int R>
+static int l3_total(int n) { return Lay<R>::total(n, Cfg<R>::NSREG); }
+
+template <int R>
+static int sweep3_occupancy(int n) {
+    const int lds = l3_total<R>(n);
+    auto kern = ame_sweep3_kernel<R>;
+    if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
+        hipSuccess)
+        return 0;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kNT, (size_t)lds) != hipSuccess)
+        return 0;
+    return per_cu;
+}
+
+int ame_sweep3_blocks_per_cu(int n, int r) {
+    switch (r) {
+#define X(RR) \
+    case RR: return sweep3_occupancy<RR>(n);
+        AME_FOR_EACH_R(X)
+#undef X
+        default: return 0;
+    }
+}
+
+// v3 needs: the slice's LDS (rings + overflow node slots) within one CU, at
+// most 2 x 31 loader DMA instructions in flight (vmcnt range) and D <= 64.
+template <int R>
+static int sweep3_fits(int n) {
+    using C = Cfg<R>;
+    if (n < 2 || C::D > 64) return 0;
+    const int ny = (n * 8 + 1023) / 1024;
+    if (2 * (ny + C::NC + 3) > 63) return 0;
+    return l3_total<R>(n) <= kLDSMAX;
+}
+
+int ame_sweep3_supported(int n, int r) {
+    switch (r) {
+#define X(RR) \
+    case RR: return sweep3_fits<RR>(n);
+        AME_FOR_EACH_R(X)
+#undef X
+        default: return 0;
+    }
+}
+
+template <int R>
+static int launch_sweep3(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {
+    const int lds = l3_total<R>(dm->n);
+    hipLaunchKernelGGL(ame_sweep3_prep_kernel<R>, dim3(dm->T_local), dim3(AME_NT), 0, st, *dm, a->x_old,
+                       a->consts, a->rinv[0], a->rinv[1], a->rinv[2], a->rinv[3], a->work);
+    if (hipGetLastError() != hipSuccess) return -3;
+    auto kern = ame_sweep3_kernel<R>;
+    if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
+        hipSuccess)
+        return -2;
+    hipLaunchKernelGGL(kern, dim3(dm->T_local), dim3(kNT), (size_t)lds, st, *dm, *a);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+int ame_sweep3_dispatch(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {
+    switch (dm->r) {
+#define X(RR) \
+    case RR: return launch_sweep3<RR>(dm, a, st);
+        AME_FOR_EACH_R(X)
+#undef X
+        default: return -1;
+    }
+}
+
+long long ame_sweep3_work_doubles(const ame_dims* dm) {
+    const long long D = 2 + 2LL * dm->r;
+    return (long long)dm->T_local * (D * D + 2LL * dm->r);
+}

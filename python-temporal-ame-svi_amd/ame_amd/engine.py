@@ -148,6 +148,10 @@ class DeviceEngine:
             if ws < 0:
                 _lib.check(-1, "ame_elbo_work_size")
             self.work = torch.empty(ws, dtype=torch.float64, device=dev)
+            sws = int(self.L.ame_sweep_work_size(ctypes.byref(self.dims)))
+            if sws < 0:
+                _lib.check(-1, "ame_sweep_work_size")
+            self.sweep_work = torch.empty(max(sws, 1), dtype=torch.float64, device=dev)
             self.out = torch.zeros(8, dtype=torch.float64, device=dev)
             self.status = torch.zeros(1, dtype=torch.int32, device=dev)
         self.epoch = 0
@@ -215,7 +219,8 @@ class DeviceEngine:
             Yt=_ptr(self.Yt), x_old=_ptr(self.x_a), x_new=_ptr(self.x_b), next_old=next_old,
             hand=_ptr(self.hand), halo_in=halo_in, halo_out=halo_out, cov=_ptr(self.cov),
             consts=_ptr(self.consts), rinv=self.C.rinv4(), lr=self.lr,
-            one_minus_lr=float(1.0 - self.lr), epoch=self.epoch, status=_ptr(self.status))
+            one_minus_lr=float(1.0 - self.lr), epoch=self.epoch, status=_ptr(self.status),
+            work=_ptr(self.sweep_work))
         tok = self._tic("sweep")
         _lib.check(self.L.ame_sweep(ctypes.byref(self.dims), ctypes.byref(a), self._sp()),
                    "ame_sweep")

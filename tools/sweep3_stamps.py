@@ -1,0 +1,85 @@
+"""Diagnostic for the v3 sweep (ame_sweep3.hip): in-kernel s_memtime stamps.
+
+    python tools/sweep3_stamps.py --build      # here: hipcc -DAME_STAMPS -> _build/libame_amd_stamps3.so
+    python tools/sweep3_stamps.py              # GPU box: config-3 sweeps, print per-wave timelines
+
+The stamped build's run time is never quoted; only its shares / timelines.
+"""
+import ctypes
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "python-temporal-ame-svi_amd")
+BDIR = os.path.join(PKG, "ame_amd", "_build")
+SO = os.path.join(BDIR, "libame_amd_stamps3.so")
+SRCS = ("ame_sweep.hip", "ame_sweep3.hip", "ame_cov.hip", "ame_elbo.hip", "ame_capi.hip",
+        "ame_selftest.hip")
+NAMES = {
+    0: ["start", "J+kj", "reduce", "ddone", "2x2+assembly", "publish", "kcnt", "brow"],
+    1: ["start", "-", "poll", "hf1", "HB", "GEMV", "-", "-", "-", "end"],
+    2: ["start", "HX", "-", "-", "HB", "GEMV", "-", "kcnt", "hf2", "end"],
+    3: ["start", "-", "-", "-", "(no HB)", "GEMV", "DMA", "kcnt", "hf2", "vmwait"],
+}
+WAVES = ["solver(w0)", "hw0(w1)", "hw3(w4)", "hw6(w7)"]
+
+
+def build(r=16):
+    os.makedirs(BDIR, exist_ok=True)
+    csrc = os.path.join(PKG, "ame_amd", "csrc")
+    defs = [f"-D{d}" for d in (" ".join(a for a in sys.argv if a.startswith("--defs=")).replace(
+        "--defs=", "")).split(",") if d]
+    objs = []
+    for src in SRCS:
+        o = os.path.join(BDIR, src.replace(".hip", "_s3.o"))
+        subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC",
+                               "-std=c++17", "-DAME_STAMPS", f"-DAME_ONLY_R={r}", *defs,
+                               "-Wno-pass-failed", "-c", os.path.join(csrc, src), "-o", o])
+        objs.append(o)
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC",
+                           "-o", SO, *objs])
+    print("built", SO)
+
+
+def run():
+    os.environ["AME_LIB_PATH"] = SO
+    sys.path.insert(0, PKG)
+    import torch
+    from ame_amd import TemporalAMEModel, TemporalAMEStructuredMFVI
+    from ame_amd import _lib
+    dev = torch.device("cuda", 0)
+    m = TemporalAMEModel(1024, 128, 16, seed=42)
+    m.generate_data_fast(device=dev)
+    vi = TemporalAMEStructuredMFVI(m, factorization="good", learning_rate=0.01, device=dev)
+    vi.fit(max_iter=2, tolerance=0.0, verbose=False)
+    torch.cuda.synchronize()
+    L = _lib.lib()
+    L.ame_debug_read_stamps3.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    st = np.zeros(4 * 16 * 16, dtype=np.uint64)
+    pg = np.zeros(256 * 5, dtype=np.uint64)
+    assert L.ame_debug_read_stamps3(st.ctypes.data, pg.ctypes.data) == 0
+    st = st.reshape(4, 16, 16).astype(np.int64)
+    pg = pg.reshape(256, 5).astype(np.int64)[:128]
+    t0 = st[0, :, 0].min()
+    print("step period (solver start-to-start), cycles:", np.diff(st[0, :, 0])[:15].tolist())
+    for w in range(4):
+        print(f"--- {WAVES[w]} (cycles after solver step start, median over 16 steps)")
+        rel = st[w] - st[0, :, 0][:, None]
+        for sl, nm in enumerate(NAMES[w]):
+            if nm == "-" or st[w, :, sl].max() == 0:
+                continue
+            print(f"  {sl:2d} {nm:14s} {int(np.median(rel[:, sl])):8d}")
+    pr = (pg - pg[:, :1]) / 100.0   # us (100 MHz realtime)
+    st0 = (pg[:, 0] - pg[0, 0]) / 100.0
+    print("lane start offset (us) at lanes 0,1,2,4,8,16,32,64,127:",
+          [round(float(st0[k]), 1) for k in (0, 1, 2, 4, 8, 16, 32, 64, 127)])
+    print("per-lane elapsed (us) to n/4, n/2, 3n/4, n; lanes 0, 64, 127:")
+    for k in (0, 64, 127):
+        print("  ", k, [round(float(x), 1) for x in pr[k, 1:]])
+
+
+if __name__ == "__main__":
+    build() if "--build" in sys.argv else run()
