@@ -47,7 +47,8 @@ using namespace ame;
 #define S3_I0 256
 __device__ unsigned long long g_s3_stamps[4 * 16 * 16];
 __device__ unsigned long long g_s3_prog[256 * 5];
-#define S3W(w) ((w) == 0 ? 0 : (w) == 1 ? 1 : (w) == 4 ? 2 : (w) == 7 ? 3 : -1)
+__device__ unsigned int g_s3_hwid[8];
+#define S3W(w) ((w) == 0 ? 0 : (w) == 1 ? 1 : (w) == 6 ? 2 : (w) == 7 ? 3 : -1)
 #define STAMP3(slot)                                                                           \
     do {                                                                                       \
         if (tl == TL / 2 && lane == 0 && i >= S3_I0 && i < S3_I0 + 16 && S3W(wave) >= 0) {     \
@@ -65,6 +66,9 @@ __device__ unsigned long long g_s3_prog[256 * 5];
             g_s3_prog[tl * 5 + q_] = __builtin_amdgcn_s_memrealtime();                         \
         }                                                                                      \
     } while (0)
+extern "C" int ame_debug_read_hwid3(unsigned int* h) {
+    return hipMemcpyFromSymbol(h, HIP_SYMBOL(g_s3_hwid), sizeof(g_s3_hwid), 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
 extern "C" int ame_debug_read_stamps3(unsigned long long* st, unsigned long long* prog) {
     if (hipMemcpyFromSymbol(st, HIP_SYMBOL(g_s3_stamps), sizeof(g_s3_stamps), 0, hipMemcpyDeviceToHost) != hipSuccess)
         return -1;
@@ -109,8 +113,10 @@ struct Lay {
     static constexpr int D = 2 + 2 * R, DD = D * D;
     static constexpr int cs = ((DD * 4 + 1023) / 1024) * 256;     // covariance ring slot (floats)
     static constexpr int oK = 0;                                   // base inverse, double buffer
-    static constexpr int oAR = al16(oK + 8 * 2 * DD);              // Qinv Phi, Phi^T Qinv (fp64)
-    static constexpr int oRec = al16(oAR + 8 * 2 * DD);            // [par][k]{L0 L1 W0 W1 G0 G1 X0 X1}
+    static constexpr int NPA = (4 * D <= 192) ? 4 : 2;
+    static constexpr int MCP = ((D + NPA - 1) / NPA) * NPA;       // AR row stride (zero padded)
+    static constexpr int oAR = al16(oK + 8 * 2 * DD);              // Qinv Phi, Phi^T Qinv (fp64) [D][MCP]
+    static constexpr int oRec = al16(oAR + 8 * 2 * D * MCP);       // [par][k]{L0 L1 W0 W1 G0 G1 X0 X1}
     static constexpr int oMu64 = al16(oRec + 8 * 2 * D * 8);       // [par][k] new mean (fp64)
     static constexpr int oMu32 = al16(oMu64 + 8 * 2 * D);          // [par][k] new mean (fp32)
     static constexpr int oG = al16(oMu32 + 4 * 2 * D);             // [node&1][k] g of node
@@ -120,9 +126,10 @@ struct Lay {
     static constexpr int oRed = al16(oDots + 8 * 32);              // solver reduction gather
     static constexpr int oGP = al16(oRed + 8 * 64);                // [node&1][wave][k] GEMV partials
     static constexpr int oYst = al16(oGP + 4 * 2 * 7 * D);         // [node&3]{y(m,m-1), y(m,m-2)} raw
-    static constexpr int oMuL = al16(oYst + 4 * 4 * 4);            // [wave][k] mu_{m,t-1}
-    static constexpr int oPd = al16(oMuL + 4 * 3 * D);             // [par][k] naive diag(P)
-    static constexpr int oFlag = al16(oPd + 8 * 2 * D);            // kcnt, ddone, gcnt
+    static constexpr int oMuL = al16(oYst + 4 * 4 * 4);            // [wave][64] mu_{m,t-1}, zero padded
+    static constexpr int oPd = al16(oMuL + 4 * 3 * 64);            // [par][k] naive diag(P)
+    static constexpr int oPc = al16(oPd + 8 * 2 * D);              // [k] diag of Pconst(t) (naive)
+    static constexpr int oFlag = al16(oPc + 8 * D);                // kcnt, ddone, gcnt
     static constexpr int oCr = al16(oFlag + 16);                   // [node&3] old covariances, DMA
     static constexpr int oXr = al16(oCr + 4 * 4 * cs);             // [node&7] old means slice t, DMA
     static constexpr int oRr = al16(oXr + 8 * 256);                // [node&3] old means slice t+1, DMA
@@ -225,13 +232,12 @@ __device__ __forceinline__ void tri_decode3(int e, int& k, int& m) {
 // J = [[1, 0, V, 0], [0, 1, 0, U]]; zero when the node does not exist.
 template <int R>
 __device__ __forceinline__ void jcol(const float* mu, bool exists, int k, double& j0, double& j1) {
-    j0 = 0.0;
-    j1 = 0.0;
-    if (!exists) return;
-    if (k == 0) j0 = 1.0;
-    else if (k == 1) j1 = 1.0;
-    else if (k < 2 + R) j0 = (double)mu[2 + R + (k - 2)];
-    else j1 = (double)mu[2 + (k - 2 - R)];
+    constexpr int D = 2 + 2 * R;
+    // branch-free: one unconditional LDS read, then selects
+    const int src = (k < 2 + R) ? (k + R) : (k - R);
+    const double v = (double)mu[(k >= 2 && k < D) ? src : 0];
+    j0 = !exists ? 0.0 : (k == 0) ? 1.0 : (k >= 2 && k < 2 + R) ? v : 0.0;
+    j1 = !exists ? 0.0 : (k == 1) ? 1.0 : (k >= 2 + R && k < D) ? v : 0.0;
 }
 
 __device__ __forceinline__ double dpp_add_xor1(double v) {
@@ -270,8 +276,9 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     using LY = Lay<R>;
     const int YS = LY::ys(n);
     double* Kbuf = (double*)(smem + LY::oK);
-    double* arQ = (double*)(smem + LY::oAR);          // Qinv Phi
-    double* arP = arQ + DD;                            // Phi^T Qinv
+    constexpr int MCP = LY::MCP;
+    double* arQ = (double*)(smem + LY::oAR);          // Qinv Phi   [D][MCP]
+    double* arP = arQ + D * MCP;                       // Phi^T Qinv [D][MCP]
     double* rec = (double*)(smem + LY::oRec);
     double* mu64 = (double*)(smem + LY::oMu64);
     float* mu32 = (float*)(smem + LY::oMu32);
@@ -284,6 +291,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     float* yst = (float*)(smem + LY::oYst);
     float* muL = (float*)(smem + LY::oMuL);
     double* pdl = (double*)(smem + LY::oPd);
+    double* pcdl = (double*)(smem + LY::oPc);
     uint32_t* flags = (uint32_t*)(smem + LY::oFlag);
     uint32_t* kcnt = flags;
     uint32_t* ddone = flags + 1;
@@ -381,9 +389,21 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         else dma16_sc1(gran_src(node) + g2, dst);
     };
 
+#ifdef AME_STAMPS
+    if (tl == TL / 2 && lane == 0) {
+        unsigned int hwid;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+        g_s3_hwid[wave] = hwid;
+    }
+#endif
     // ============================ prologue ============================
     for (int e = tid; e < DD; e += kNT) Kbuf[e] = K0[e];
-    for (int e = tid; e < 2 * DD; e += kNT) arQ[e] = QiPhi[e];   // QiPhi, PhiTQi are adjacent
+    for (int e = tid; e < 2 * D * MCP; e += kNT) {   // QiPhi, PhiTQi (adjacent in consts), padded
+        const int mat = e / (D * MCP), rc = e - mat * D * MCP, rr = rc / MCP, cc = rc - rr * MCP;
+        arQ[e] = (cc < D) ? QiPhi[(size_t)mat * DD + rr * D + cc] : 0.0;
+    }
+    for (int e = tid; e < 3 * 64; e += kNT) muL[e] = 0.f;
+    if (tid < D) pcdl[tid] = pconst_entry(a.consts, D, tid, tid, tg, Tt);
     for (int e = tid; e < 2 * D * 8; e += kNT) rec[e] = 0.0;
     for (int e = tid; e < 2 * D; e += kNT) {
         mu64[e] = 0.0;
@@ -434,33 +454,38 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         float acc[D];
 #pragma unroll
         for (int c = 0; c < D; ++c) acc[c] = 0.f;
+        float2 yv[NSREG];
+#pragma unroll
+        for (int s = 0; s < NSREG; ++s) {   // ring slots are >= n long: loads need no guard
+            const int j = hl + kNH * s;
+            const float2 y = ysrc[j];
+            yv[s] = (j < n) ? y : make_float2(0.f, 0.f);
+        }
 #pragma unroll
         for (int s = 0; s < NSREG; ++s) {
             if (s < ns) {
                 const int j = hl + kNH * s;
-                const float2 y = (j < n) ? ysrc[j] : make_float2(0.f, 0.f);
-                if (j == m - 1) { yst[(m & 3) * 4 + 0] = y.x; yst[(m & 3) * 4 + 1] = y.y; }
-                if (j == m - 2) { yst[(m & 3) * 4 + 2] = y.x; yst[(m & 3) * 4 + 3] = y.y; }
-                float z0 = r00f * y.x + r01f * y.y;
-                float z1 = r10f * y.x + r11f * y.y;
-                if (j >= m - 2 && j <= m) { z0 = 0.f; z1 = 0.f; }
+                const bool ex = (j >= m - 2) && (j <= m);
+                const float z0 = ex ? 0.f : r00f * yv[s].x + r01f * yv[s].y;
+                const float z1 = ex ? 0.f : r10f * yv[s].x + r11f * yv[s].y;
                 acc[0] += z0;
                 acc[1] += z1;
+#ifndef AME_ABL_GEMV_NOFMA
 #pragma unroll
                 for (int c = 0; c < R; ++c) {
                     acc[2 + c] = fmaf(z0, mreg[s][R + c], acc[2 + c]);       // h_U += z0 V
                     acc[2 + R + c] = fmaf(z1, mreg[s][c], acc[2 + R + c]);   // h_V += z1 U
                 }
+#endif
             }
         }
         for (int s = NSREG; s < ns; ++s) {
             const int j = hl + kNH * s;
-            const float2 y = (j < n) ? ysrc[j] : make_float2(0.f, 0.f);
-            if (j == m - 1) { yst[(m & 3) * 4 + 0] = y.x; yst[(m & 3) * 4 + 1] = y.y; }
-            if (j == m - 2) { yst[(m & 3) * 4 + 2] = y.x; yst[(m & 3) * 4 + 3] = y.y; }
-            float z0 = r00f * y.x + r01f * y.y;
-            float z1 = r10f * y.x + r11f * y.y;
-            if (j >= m - 2 && j <= m) { z0 = 0.f; z1 = 0.f; }
+            float2 y = ysrc[j];
+            if (j >= n) y = make_float2(0.f, 0.f);
+            const bool ex = (j >= m - 2) && (j <= m);
+            const float z0 = ex ? 0.f : r00f * y.x + r01f * y.y;
+            const float z1 = ex ? 0.f : r10f * y.x + r11f * y.y;
             acc[0] += z0;
             acc[1] += z1;
             const float2* ml = mlds + (size_t)(s - NSREG) * MP * kNH + hl;
@@ -474,66 +499,76 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                     if (c + 1 < R) acc[2 + R + c + 1] = fmaf(z1, t.y, acc[2 + R + c + 1]);
                     else acc[2 + (c + 1 - R)] = fmaf(z0, t.y, acc[2 + (c + 1 - R)]);
                 }
-                if ((c2 & 3) == 3) asm volatile("" ::: "memory");
             }
         }
         int idx;
+#ifndef AME_ABL_GEMV_NORED
         const float v = wave_reduce_scatter<D>(acc, lane, idx);
+#else
+        const float v = acc[lane % D]; idx = lane;
+#endif
         if (idx < D) gp[((m & 1) * 7 + hw) * D + idx] = v;
+        // raw y_{m,m-1}, y_{m,m-2} for the solver / HF1 (owner lanes only)
+        const int jm1 = m - 1, jm2 = m - 2;
+        if (jm1 >= 0 && (jm1 % kNH) == hl) {
+            const float2 y = ysrc[jm1];
+            yst[(m & 3) * 4 + 0] = y.x;
+            yst[(m & 3) * 4 + 1] = y.y;
+        }
+        if (jm2 >= 0 && (jm2 % kNH) == hl) {
+            const float2 y = ysrc[jm2];
+            yst[(m & 3) * 4 + 2] = y.x;
+            yst[(m & 3) * 4 + 3] = y.y;
+        }
     };
     // HF1 (hw 0..2): AR terms + natural parameter g of node m.
     // mu_{m,t-1} in muL[hw], mu_{m,t+1}^old in rring[m&3].
     auto hf1 = [&](int m) {
         const int q = hl;   // 0..191
         const int k = q / NP, p = q - k * NP;
-        double acc = 0.0;
-        if (k < D) {
-            const float* ml = muL + hw * D;
-            const float* mr = rring + (m & 3) * 64;
+        const int kc = (k < D) ? k : 0;
+        const float* ml = muL + hw * 64;          // zero beyond D; zero when tg == 0
+        const float* mr = rring + (m & 3) * 64;   // finite beyond D (padded coefficients are 0)
+        const double* aq = arQ + kc * MCP + p * MC;
+        const double* ap = arP + kc * MCP + p * MC;
+        double accL = 0.0, accR = 0.0;
 #pragma unroll
-            for (int mm = 0; mm < MC; ++mm) {
-                const int c = p * MC + mm;
-                if (c < D) {
-                    if (tg > 0) acc = fma(arQ[k * D + c], (double)ml[c], acc);
-                    if (tg < Tt - 1) acc = fma(arP[k * D + c], (double)mr[c], acc);
-                }
-            }
+        for (int mm = 0; mm < MC; ++mm) {
+            const int c = p * MC + mm;
+            accL = fma(aq[mm], (double)ml[c], accL);
+            accR = fma(ap[mm], (double)mr[c], accR);
         }
+        double acc = accL + ((tg < Tt - 1) ? accR : 0.0);
         acc = dpp_add_xor1(acc);
         if constexpr (NP == 4) acc = dpp_add_mirror4(acc);
-        if (k < D && p == 0) {
-            double g = 0.0;
+        // lane (k, 0) assembles g_k = GEMV partials + AR + node m-2's term
+        double g = 0.0;
 #pragma unroll
-            for (int w = 0; w < 7; ++w) g += (double)gp[((m & 1) * 7 + w) * D + k];
-            g += acc;
-            if (m >= 2) {   // node m-2 was excluded from the GEMV; its new mean is known now
-                const float* mup = mu32 + ((m - 2) & 1) * D;
-                double j0, j1;
-                jcol<R>(mup, true, k, j0, j1);
-                const double y0 = (double)yst[(m & 3) * 4 + 2], y1 = (double)yst[(m & 3) * 4 + 3];
-                const double z0 = r00 * y0 + r01 * y1, z1 = r10 * y0 + r11 * y1;
-                g = fma(j0, z0, fma(j1, z1, g));
-            }
-            g64[(m & 1) * D + k] = g;
+        for (int w = 0; w < 7; ++w) g += (double)gp[((m & 1) * 7 + w) * D + kc];
+        g += acc;
+        if (m >= 2) {   // node m-2 was excluded from the GEMV; its new mean is known now
+            const float* mup = mu32 + ((m - 2) & 1) * D;
+            double j0, j1;
+            jcol<R>(mup, true, kc, j0, j1);
+            const double y0 = (double)yst[(m & 3) * 4 + 2], y1 = (double)yst[(m & 3) * 4 + 3];
+            const double z0 = r00 * y0 + r01 * y1, z1 = r10 * y0 + r11 * y1;
+            g = fma(j0, z0, fma(j1, z1, g));
         }
+        if (k < D && p == 0) g64[(m & 1) * D + k] = g;
     };
     // HF2 (hw 3..6): v = K g, yv = K Jn^T for node m with base Kb
     auto hf2 = [&](int m, const double* Kb) {
         const int q = tid - 256;
         const int k = q / (3 * NHALF), rem = q - k * (3 * NHALF);
         const int vsel = rem / NHALF, half = rem - vsel * NHALF;
-        double acc = 0.0, accA = 0.0;
-        if (k < D) {
-            const double* vec = (vsel == 0) ? g64 + (m & 1) * D : jn64 + (vsel - 1) * D;
-            const double* kr = Kb + (size_t)k * D;
-            const int c0 = half * HD;
+        const int kc = (k < D) ? k : 0;
+        const double* vec = (vsel == 0) ? g64 + (m & 1) * D : jn64 + (vsel - 1) * D;
+        const double* kr = Kb + (size_t)kc * D;
+        const int c0 = half * HD;
+        double acc = 0.0;
 #pragma unroll
-            for (int c = 0; c < HD; ++c) {
-                acc = fma(kr[c0 + c], vec[c0 + c], acc);
-                if ((c & 3) == 3) asm volatile("" ::: "memory");
-            }
-            if (vsel == 0 && half == 0) accA = kr[0] * vec[0] + kr[1] * vec[1];
-        }
+        for (int c = 0; c < HD; ++c) acc = fma(kr[c0 + c], vec[c0 + c], acc);
+        const double accA = kr[0] * vec[0] + kr[1] * vec[1];
         if constexpr (NHALF == 2) acc = dpp_add_xor1(acc);
         if (k < D && half == 0) {
             double* vo = vbuf + ((m & 1) * D + k) * 4;
@@ -558,7 +593,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             uint64_t g0 = 0;
             if (tg > 0 && lane < D)
                 g0 = (tl == 0) ? gran_load_system(gran_src(0) + lane) : gran_load_agent(gran_src(0) + lane);
-            gran_finish(0, g0, muL + hw * D);
+            gran_finish(0, g0, muL + hw * 64);
         }
         if (hw == 3) jn_fill(1);
     }
@@ -576,9 +611,12 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
 
     if (wave == 0) {
         // ============================ SOLVER ============================
+#ifndef AME_ABL_NOPRIO
         __builtin_amdgcn_s_setprio(3);
+#endif
         const int k = lane;
         const bool kl = k < D;
+        const int kc = kl ? k : 0;
         double brow[D];   // row k of the base inverse B_i
 #pragma unroll
         for (int c = 0; c < D; ++c) brow[c] = kl ? Kbuf[(size_t)k * D + c] : 0.0;
@@ -591,14 +629,12 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             const bool has_prev = i > 0;
             const float* mup = mu32 + ppar * D;       // mu_{i-1} (fp32)
             const double* mupd = mu64 + ppar * D;     // mu_{i-1} (fp64)
-            double v = 0, yv0 = 0, yv1 = 0, vA = 0, g = 0;
-            if (kl) {
-                const double* vi = vbuf + (par * D + k) * 4;
-                v = vi[0]; yv0 = vi[1]; yv1 = vi[2]; vA = vi[3];
-                g = g64[par * D + k];
-            }
-            double J0 = 0, J1 = 0;
-            if (kl) jcol<R>(mup, has_prev, k, J0, J1);
+            const double msk = kl ? 1.0 : 0.0;
+            const double* vi = vbuf + (par * D + kc) * 4;
+            const double v = msk * vi[0], yv0 = msk * vi[1], yv1 = msk * vi[2], vA = msk * vi[3];
+            const double g = msk * g64[par * D + kc];
+            double J0, J1;
+            jcol<R>(mup, has_prev && kl, kc, J0, J1);
             // kj = B J^T (the one critical matvec)
             double kj0 = 0, kj1 = 0;
             if (has_prev) {
@@ -729,7 +765,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                         const double oo = (k < 2 + R) ? (double)xold[k + R] : (double)xold[k - R];
                         pd = ((k < 2 + R) ? p : s) * (sq_other - oo * oo);
                     }
-                    pdl[par * D + k] = pd + pconst_entry(a.consts, D, k, k, tg, Tt);
+                    pdl[par * D + k] = pd + pcdl[k];
                     const double mo = (double)mold, mn = (double)nw;
                     if (k >= 2) ssq_l = ssq_l - mo * mo + mn * mn;
                 }
@@ -770,26 +806,25 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             const int par = i & 1, ppar = (i + 1) & 1;
             const double* Bi = Kbuf + (size_t)par * DD;      // B_i
             double* Kn = Kbuf + (size_t)ppar * DD;           // K_i = B_{i+1}
-            // HX (hw 3): dots that do not involve mu_{i-1}
-            if (hw == 3 && i < n) {
+            // HX (hw 5, off the solver's SIMD): dots that do not involve mu_{i-1}
+            if (hw == 5 && i < n) {
                 const int k = lane;
+                const int kc = (k < D) ? k : 0;
+                const double msk = (k < D) ? 1.0 : 0.0;
+                const double* rc = rec + (ppar * D + kc) * 8;
+                const double W0 = msk * rc[2], W1 = msk * rc[3], X0 = msk * rc[6], X1 = msk * rc[7];
+                const double g = g64[par * D + kc];
+                const double yv0 = vbuf[(par * D + kc) * 4 + 1], yv1 = vbuf[(par * D + kc) * 4 + 2];
+                double n0, n1;
+                jcol<R>(xring + ((i + 1) & 7) * 64, i + 1 < n, kc, n0, n1);
+                const double gA = (k < 2) ? g : 0.0;
                 double pr[20];
-#pragma unroll
-                for (int q = 0; q < 20; ++q) pr[q] = 0.0;
-                if (k < D) {
-                    const double* rc = rec + (ppar * D + k) * 8;
-                    const double W0 = rc[2], W1 = rc[3], X0 = rc[6], X1 = rc[7];
-                    const double g = g64[par * D + k];
-                    const double yv0 = vbuf[(par * D + k) * 4 + 1], yv1 = vbuf[(par * D + k) * 4 + 2];
-                    double n0, n1;
-                    jcol<R>(xring + ((i + 1) & 7) * 64, i + 1 < n, k, n0, n1);
-                    const double gA = (k < 2) ? g : 0.0;
-                    pr[0] = W0 * g; pr[1] = W1 * g; pr[2] = X0 * g; pr[3] = X1 * g;           // b1, b2
-                    pr[4] = W0 * n0; pr[5] = W0 * n1; pr[6] = W1 * n0; pr[7] = W1 * n1;       // f1[p][q]
-                    pr[8] = X0 * n0; pr[9] = X0 * n1; pr[10] = X1 * n0; pr[11] = X1 * n1;     // f2[p][q]
-                    pr[12] = n0 * yv0; pr[13] = n0 * yv1; pr[14] = n1 * yv0; pr[15] = n1 * yv1; // ny[q][p]
-                    pr[16] = W0 * gA; pr[17] = W1 * gA; pr[18] = X0 * gA; pr[19] = X1 * gA;   // b1A, b2A
-                }
+                pr[0] = W0 * g; pr[1] = W1 * g; pr[2] = X0 * g; pr[3] = X1 * g;           // b1, b2
+                pr[4] = W0 * n0; pr[5] = W0 * n1; pr[6] = W1 * n0; pr[7] = W1 * n1;       // f1[p][q]
+                pr[8] = X0 * n0; pr[9] = X0 * n1; pr[10] = X1 * n0; pr[11] = X1 * n1;     // f2[p][q]
+                pr[12] = msk * n0 * yv0; pr[13] = msk * n0 * yv1;                          // ny[q][p]
+                pr[14] = msk * n1 * yv0; pr[15] = msk * n1 * yv1;
+                pr[16] = W0 * gA; pr[17] = W1 * gA; pr[18] = X0 * gA; pr[19] = X1 * gA;   // b1A, b2A
                 int idx;
                 const double sv = wave_reduce_scatter<20>(pr, lane, idx);
                 if (idx < 20) dots[idx] = sv;
@@ -804,27 +839,31 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 float* cv = cvs + (size_t)(i > 0 ? i - 1 : 0) * DD;
 #pragma unroll
                 for (int q = 0; q < LTQ; ++q) {
-                    const int k = lk[q], m = lm[q];
-                    if (k < 0) continue;
+                    const bool ok = lk[q] >= 0;
+                    const int k = ok ? lk[q] : 0, m = ok ? lm[q] : 0;
                     const double* rk = rp + k * 8;
                     const double* rm = rp + m * 8;
-                    const double c = Bi[k * D + m] - (rk[0] * rm[2] + rk[1] * rm[3]);
-                    if (i < n) {
-                        const double kn = c + (rk[4] * rm[6] + rk[5] * rm[7]);
+                    const double bkm = Bi[k * D + m];
+                    const float ckm = co[k * D + m], cmk = co[m * D + k];
+                    const double c = bkm - (rk[0] * rm[2] + rk[1] * rm[3]);
+                    const double kn = c + (rk[4] * rm[6] + rk[5] * rm[7]);
+                    float c32;
+                    if (is_naive) {
+                        c32 = (k == m) ? 1.0f / ((float)pdp[k] + 1e-8f) : 0.f;
+                    } else {
+                        c32 = (float)c;
+                        if (is_bad && ((k < 2) != (m < 2))) c32 = 0.f;
+                        if (k == m) c32 = c32 + 1e-6f;
+                    }
+                    const float n_km = __fadd_rn(__fmul_rn(lr, c32), __fmul_rn(om, ckm));
+                    const float n_mk = __fadd_rn(__fmul_rn(lr, c32), __fmul_rn(om, cmk));
+                    if (ok && i < n) {
                         Kn[k * D + m] = kn;
                         Kn[m * D + k] = kn;
                     }
-                    if (i >= 1) {
-                        float c32;
-                        if (is_naive) {
-                            c32 = (k == m) ? 1.0f / ((float)pdp[k] + 1e-8f) : 0.f;
-                        } else {
-                            c32 = (float)c;
-                            if (is_bad && ((k < 2) != (m < 2))) c32 = 0.f;
-                            if (k == m) c32 = c32 + 1e-6f;
-                        }
-                        cv[k * D + m] = __fadd_rn(__fmul_rn(lr, c32), __fmul_rn(om, co[k * D + m]));
-                        if (k != m) cv[m * D + k] = __fadd_rn(__fmul_rn(lr, c32), __fmul_rn(om, co[m * D + k]));
+                    if (ok && i >= 1) {
+                        cv[k * D + m] = n_km;
+                        if (k != m) cv[m * D + k] = n_mk;
                     }
                 }
             }
@@ -834,7 +873,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             if (hw <= 2 && i + 1 < n) {
                 uint64_t gv = 0;
                 if (lane < D) gv = pring[(size_t)((i + 1) & 3) * 128 + lane];
-                gran_finish(i + 1, gv, muL + hw * D);
+                gran_finish(i + 1, gv, muL + hw * 64);
                 STAMP3(2);
                 wave_lds_sync3();
                 hf1(i + 1);

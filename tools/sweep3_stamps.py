@@ -15,7 +15,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "python-temporal-ame-svi_amd")
 BDIR = os.path.join(PKG, "ame_amd", "_build")
-SO = os.path.join(BDIR, "libame_amd_stamps3.so")
+TAG = ([a.split("=", 1)[1] for a in sys.argv if a.startswith("--tag=")] or [""])[0]
+SO = os.path.join(BDIR, f"libame_amd_stamps3{TAG}.so")
 SRCS = ("ame_sweep.hip", "ame_sweep3.hip", "ame_cov.hip", "ame_elbo.hip", "ame_capi.hip",
         "ame_selftest.hip")
 NAMES = {
@@ -24,7 +25,7 @@ NAMES = {
     2: ["start", "HX", "-", "-", "HB", "GEMV", "-", "kcnt", "hf2", "end"],
     3: ["start", "-", "-", "-", "(no HB)", "GEMV", "DMA", "kcnt", "hf2", "vmwait"],
 }
-WAVES = ["solver(w0)", "hw0(w1)", "hw3(w4)", "hw6(w7)"]
+WAVES = ["solver(w0)", "hw0(w1)", "hw5(w6)", "hw6(w7)"]
 
 
 def build(r=16):
@@ -34,7 +35,7 @@ def build(r=16):
         "--defs=", "")).split(",") if d]
     objs = []
     for src in SRCS:
-        o = os.path.join(BDIR, src.replace(".hip", "_s3.o"))
+        o = os.path.join(BDIR, src.replace(".hip", f"_s3{TAG}.o"))
         subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC",
                                "-std=c++17", "-DAME_STAMPS", f"-DAME_ONLY_R={r}", *defs,
                                "-Wno-pass-failed", "-c", os.path.join(csrc, src), "-o", o])
@@ -62,6 +63,11 @@ def run():
     pg = np.zeros(256 * 5, dtype=np.uint64)
     assert L.ame_debug_read_stamps3(st.ctypes.data, pg.ctypes.data) == 0
     st = st.reshape(4, 16, 16).astype(np.int64)
+    L.ame_debug_read_hwid3.argtypes = [ctypes.c_void_p]
+    hw = np.zeros(8, dtype=np.uint32)
+    L.ame_debug_read_hwid3(hw.ctypes.data)
+    print("HW_ID per wave (wave_id, simd_id, cu_id):",
+          [(int(h & 15), int((h >> 4) & 3), int((h >> 8) & 15)) for h in hw])
     pg = pg.reshape(256, 5).astype(np.int64)[:128]
     t0 = st[0, :, 0].min()
     print("step period (solver start-to-start), cycles:", np.diff(st[0, :, 0])[:15].tolist())
