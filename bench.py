@@ -39,9 +39,10 @@ def kernel_bytes(n, TL, d, swap_consistent=True):
     y_full = 8.0 * n * (n - 1) * TL
     return {
         # Y row of every ordered dyad + old means read + new means written
-        "sweep": y_full + 8.0 * n * TL * d,
-        # old covariance read + new written + old/new means read
-        "cov": 8.0 * n * TL * d * d + 8.0 * n * TL * d,
+        # + old covariance read + damped covariance written
+        "sweep": y_full + 8.0 * n * TL * d + 8.0 * n * TL * d * d,
+        # each covariance read once
+        "cov": 4.0 * n * TL * d * d,
         # Y (upper triangle if swap-consistent) + means
         "elbo": (y_full / 2 if swap_consistent else y_full) + 4.0 * n * TL * d,
     }

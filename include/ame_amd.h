@@ -73,7 +73,8 @@ typedef struct ame_sweep_args {
     const uint64_t* halo_in;     /* [n][d] granules of slice t_begin-1 (left rank), or NULL */
     uint64_t* halo_out;          /* [n][d] granules of slice t_begin+T_local-1 for the right
                                     rank (peer/host-mapped), or NULL */
-    float* cov;                  /* [T_local][n][d][d] covariances, damped in place */
+    float* cov;                  /* [T_local][n][d][d] covariances before the sweep (damped in
+                                    place when cov_new is NULL) */
     const double* consts;        /* fp64 [5][d][d] */
     double rinv[4];              /* R_inv row-major (host values) */
     float lr;                    /* learning_rate (damping) */
@@ -82,6 +83,9 @@ typedef struct ame_sweep_args {
     uint32_t* status;            /* [1] error word */
     double* work;                /* scratch, >= ame_sweep_work_size() doubles (per-slice base
                                     inverse and column sums of squares) */
+    float* cov_new;              /* [T_local][n][d][d] damped covariances after the sweep, or NULL
+                                    (in place).  A separate buffer lets ame_cov / ame_elbo read
+                                    `cov` while the next sweep already runs (engine speculation) */
 } ame_sweep_args;
 
 typedef struct ame_cov_args {
@@ -127,7 +131,7 @@ int ame_sweep_max_slices(int n, int r);
 long long ame_sweep_lds_bytes(int n, int r);
 
 /* Per-(node, local slice) covariance terms of the ELBO (log|S|, tr S,
- * tr(Qinv S), tr(S0inv S)), fully parallel: one wave per covariance. */
+ * tr(Qinv S), tr(S0inv S)), fully parallel: 64/(2r) covariances per wave. */
 int ame_cov(const ame_dims* dims, const ame_cov_args* args, void* stream);
 
 /* ELBO / reconstruction sufficient sums over the local slices:

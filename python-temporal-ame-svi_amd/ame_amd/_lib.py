@@ -31,7 +31,7 @@ class ame_sweep_args(ctypes.Structure):
                 ("hand", c_vp), ("halo_in", c_vp), ("halo_out", c_vp), ("cov", c_vp),
                 ("consts", c_vp), ("rinv", ctypes.c_double * 4), ("lr", ctypes.c_float),
                 ("one_minus_lr", ctypes.c_float), ("epoch", ctypes.c_uint32), ("status", c_vp),
-                ("work", c_vp)]
+                ("work", c_vp), ("cov_new", c_vp)]
 
 
 class ame_cov_args(ctypes.Structure):

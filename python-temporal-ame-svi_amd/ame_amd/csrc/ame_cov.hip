@@ -1,108 +1,143 @@
-// K1b: per-(node,time) covariance terms of the ELBO.
+// K2: per-(node,time) covariance terms of the ELBO.
 //
 // Reference: entropy logdet (structured_mf.py:202-209), the trace correction of
 // the expected log-likelihood (:142-144), tr(S0^-1 S_i0) (:166) and
-// tr(Q^-1 S_it) (:193).  The covariances themselves are written by the sweep
-// (ame_sweep.hip); this kernel reads each stored fp32 covariance once.
+// tr(Q^-1 S_it) (:193).  The covariances are written by the sweep; this kernel
+// reads each stored fp32 covariance once (4 d^2 bytes).
 //
-// One wave per (node, slice), column-per-lane fp64 registers (lane m holds
-// column m).  log|S| is the sum of log pivots of a forward elimination
-// (LDL^T), torch.logdet semantics for indefinite input.  Pivot steps are
-// template-recursive so every register index is a compile-time constant.
+// Work split (x = [a, b, U(r), V(r)], d = 2 + 2r):
+//  * the (a,b) 2x2 block is eliminated first with its closed-form inverse,
+//    leaving the 2r x 2r Schur complement S = A_xx - A_xa A_aa^-1 A_ax;
+//  * S is factorised LDL^T with column c of S in lane c, so 64 / 2r
+//    covariances share a wave (2 at r = 16) and no lane idles; the pivot row
+//    goes through LDS (one store per lane, broadcast reads back).
+// The input is taken as symmetric: the sweep writes symmetric covariances and
+// the reference's initialisation symmetrises (structured_mf.py:94-96).
+// log|A| = log|A_aa| + sum log pivots, accumulated as one product with
+// periodic exponent extraction (one log per covariance); torch.logdet
+// semantics: -inf for a zero pivot, nan for a negative determinant.
 #include "ame_common.h"
 
-// Bound the scheduler's load hoisting inside fully-unrolled D-loops: without it
-// hipcc issues every global/LDS load of the loop up front (>400 registers).
-#define AME_CHUNK(k) \
-    if (((k) & 3) == 3) asm volatile("" ::: "memory")
-
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// Forward elimination of pivot P (and all later ones): accumulates log|piv|.
-template <int D, int P>
-__device__ __forceinline__ void elim_from(double (&col)[D], double* row, int lane, double& ld,
-                                          int& neg, bool& zero) {
-    if constexpr (P < D) {
-        row[lane] = col[P];
-        wave_sync();
-        const double piv = row[P];
-        zero |= (piv == 0.0);
-        neg ^= (piv < 0.0) ? 1 : 0;
-        ld += log(fabs(piv));
-        const double f = (lane > P) ? col[P] / piv : 0.0;
-#pragma unroll
-        for (int k0 = P + 1; k0 < D; k0 += 4) {
-#pragma unroll
-            for (int k = k0; k < k0 + 4 && k < D; ++k) col[k] = fma(-row[k], f, col[k]);
-            asm volatile("" ::: "memory");
-        }
-        wave_sync();
-        elim_from<D, P + 1>(col, row, lane, ld, neg, zero);
-    }
-}
-
+template <int B>
+struct CovLanes {   // lanes per covariance: next power of two >= 2r
+    static constexpr int v = B <= 2 ? 2 : B <= 4 ? 4 : B <= 8 ? 8 : B <= 16 ? 16 : B <= 32 ? 32 : 64;
+};
 
 template <int R>
 __global__ void __launch_bounds__(AME_NT)
 ame_cov_kernel(ame_dims dm, ame_cov_args a) {
-    constexpr int D = 2 + 2 * R;
-    const int n = dm.n;
-    const int per = (n + 3) / 4;
-    const int tl = blockIdx.x / per;
-    const int i = (blockIdx.x - tl * per) * 4 + (threadIdx.x >> 6);
+    constexpr int D = 2 + 2 * R, B = 2 * R, DD = D * D;
+    constexpr int LPM = CovLanes<B>::v, MPW = 64 / LPM, WPB = AME_NT / 64;
+    __shared__ double qs[2 * DD];                                   // S0inv, Qinv
+    __shared__ __attribute__((aligned(16))) double rows[WPB][64];   // pivot rows
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (int e = tid; e < 2 * DD; e += AME_NT) qs[e] = a.consts[e];
+    __syncthreads();
+    const long long total = (long long)dm.T_local * dm.n;
+    const long long first = ((long long)blockIdx.x * WPB + w) * MPW;
+    if (first >= total) return;   // whole wave; no barrier follows
+    const int sub = lane / LPM, l = lane - sub * LPM;
+    const bool mv = first + sub < total;
+    const long long mc = mv ? first + sub : total - 1;
+    const int tl = (int)(mc / dm.n);
     const int tg = dm.t_begin + tl;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    __shared__ double rows[AME_NT / 64][64];
-    if (i >= n) return;   // whole wave exits; no workgroup barrier below
-    const size_t DD = (size_t)D * D;
-    const bool mlane = lane < D;
-    const float* cv = a.cov + (((size_t)tl * n + i) * D) * D;
-    const double* consts = a.consts;
-    int m = mlane ? lane : 0;
-    asm volatile("" : "+s"(consts));
-    asm volatile("" : "+v"(m), "+v"(cv));
-    double col[D];
+    const bool lv = l < B;
+    const int c = 2 + (lv ? l : 0);
+    const float* A = a.cov + mc * DD;
+    const double* S0 = qs;
+    const double* Qi = qs + DD;
+
+    // the (a,b) block and this lane's column c in rows 0, 1
+    const double a00 = A[0], a01 = A[1], a10 = A[D], a11 = A[D + 1];
+    const double u0 = A[c], u1 = A[D + c];
+    const double det2 = a00 * a11 - a01 * a10;
+    const double id2 = 1.0 / det2;
+    const double w0 = (a11 * u0 - a01 * u1) * id2;   // A_aa^-1 (A_0c, A_1c)
+    const double w1 = (a00 * u1 - a10 * u0) * id2;
+    // traces: column c (rows 0, 1 here, rows >= 2 in the loop) and columns 0, 1
+    // (every lane computes them, lane l == 0 keeps them)
+    double tq = Qi[c] * u0 + Qi[D + c] * u1;
+    double tq0 = Qi[0] * a00 + Qi[1] * a10 + Qi[D] * a01 + Qi[D + 1] * a11;
+    double tr = 0.0;
+    double col[B];
 #pragma unroll
-    for (int k = 0; k < D; ++k) {
-        col[k] = mlane ? (double)cv[(size_t)k * D + m] : 0.0;
-        AME_CHUNK(k);
+    for (int k = 0; k < B; ++k) {
+        const float* rk = A + (2 + k) * D;
+        const double x = rk[c], c0 = rk[0], c1 = rk[1];
+        tq = fma(Qi[(2 + k) * D + c], x, tq);
+        tr = (k == l) ? x : tr;
+        tq0 = fma(Qi[2 + k], c0, fma(Qi[D + 2 + k], c1, tq0));
+        col[k] = x - (c0 * w0 + c1 * w1);
+        if ((k & 7) == 7) asm volatile("" ::: "memory");
     }
-    double tr = 0.0, trq = 0.0, trs = 0.0;
-    if (mlane) {
-#pragma unroll
-        for (int k = 0; k < D; ++k) {
-            if (k == m) tr = col[k];
-            trq = fma(consts[DD + (size_t)k * D + m], col[k], trq);
-            if (tg == 0) trs = fma(consts[(size_t)k * D + m], col[k], trs);
-            AME_CHUNK(k);
+    double ts = 0.0;
+    if (__any(tg == 0)) {   // tr(S0inv A): first time slice only (wave-uniform branch)
+        ts = S0[c] * u0 + S0[D + c] * u1;
+        double ts0 = S0[0] * a00 + S0[1] * a10 + S0[D] * a01 + S0[D + 1] * a11;
+        for (int k = 0; k < B; ++k) {
+            const float* rk = A + (2 + k) * D;
+            ts = fma(S0[(2 + k) * D + c], (double)rk[c], ts);
+            ts0 = fma(S0[2 + k], (double)rk[0], fma(S0[D + 2 + k], (double)rk[1], ts0));
         }
+        if (l == 0) ts += ts0;
     }
-    double ld = 0.0;
-    int neg = 0;
-    bool zero = false;
-    elim_from<D, 0>(col, rows[w], lane, ld, neg, zero);
+
+    // LDL^T of the complement: lane c holds column c; pivot row through LDS
+    double* rb = rows[w] + sub * LPM;
+    double prod = det2;
+    int e2 = 0, neg = det2 < 0.0 ? 1 : 0;
+    bool zero = det2 == 0.0;
+#pragma unroll
+    for (int P = 0; P < B; ++P) {
+        rb[l] = col[P];
+        asm volatile("" ::: "memory");   // one wave: its LDS ops complete in issue order
+        const double piv = rb[P];
+        zero |= piv == 0.0;
+        neg ^= piv < 0.0 ? 1 : 0;
+        prod *= piv;
+        if ((P & 7) == 7 || P == B - 1) {
+            int ex;
+            prod = frexp(prod, &ex);
+            e2 += ex;
+        }
+        double ri = __builtin_amdgcn_rcp(piv);
+        ri = fma(fma(-piv, ri, 1.0), ri, ri);
+        ri = fma(fma(-piv, ri, 1.0), ri, ri);
+        const double f = col[P] * ri;
+#pragma unroll
+        for (int k = P + 1; k < B; ++k) col[k] = fma(-rb[k], f, col[k]);
+        asm volatile("" ::: "memory");
+    }
+    double ld = log(fabs(prod)) + (double)e2 * 0.69314718055994530942;
     if (zero) ld = -INFINITY;
     else if (neg) ld = NAN;
-    tr = wave_sum(tr);
-    trq = wave_sum(trq);
-    trs = wave_sum(trs);
-    if (lane == 0) {
-        double* o = a.cov_terms + ((size_t)tl * n + i) * 4;
+
+    double s_tr = lv ? tr : 0.0, s_tq = lv ? tq : 0.0, s_ts = lv ? ts : 0.0;
+    if (l == 0) {
+        s_tr += a00 + a11;
+        s_tq += tq0;
+    }
+#pragma unroll
+    for (int o = 1; o < LPM; o <<= 1) {
+        s_tr += __shfl_xor(s_tr, o);
+        s_tq += __shfl_xor(s_tq, o);
+        s_ts += __shfl_xor(s_ts, o);
+    }
+    if (l == 0 && mv) {
+        double* o = a.cov_terms + mc * 4;
         o[0] = ld;
-        o[1] = tr;
-        o[2] = (tg >= 1) ? trq : 0.0;
-        o[3] = (tg == 0) ? trs : 0.0;
+        o[1] = s_tr;
+        o[2] = (tg >= 1) ? s_tq : 0.0;
+        o[3] = (tg == 0) ? s_ts : 0.0;
     }
 }
 
 template <int R>
 static int launch_cov(const ame_dims* dm, const ame_cov_args* a, hipStream_t st) {
-    const int per = (dm->n + 3) / 4;
-    hipLaunchKernelGGL(ame_cov_kernel<R>, dim3(dm->T_local * per), dim3(AME_NT), 0, st, *dm, *a);
+    constexpr int per_block = (AME_NT / 64) * (64 / CovLanes<2 * R>::v);
+    const long long total = (long long)dm->T_local * dm->n;
+    const long long blocks = (total + per_block - 1) / per_block;
+    hipLaunchKernelGGL(ame_cov_kernel<R>, dim3((unsigned)blocks), dim3(AME_NT), 0, st, *dm, *a);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -174,6 +174,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     const float* xo = a.x_old + (size_t)tl * n * D;
     float* xn = a.x_new + (size_t)tl * n * D;
     float* cvs = a.cov + (size_t)tl * n * DD;
+    float* cvw = (a.cov_new != nullptr ? a.cov_new : a.cov) + (size_t)tl * n * DD;   // damped output
     const float* ysl = a.Yt + (size_t)tl * n * n * 2;
     const float lr = a.lr, om = a.one_minus_lr;
     bool dead = false;
@@ -620,7 +621,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         STAMP(2);
         // ---------------- phase 3 ----------------
         {
-            float* cv = cvs + (size_t)i * DD;
+            float* cv = cvw + (size_t)i * DD;
 #pragma unroll
             for (int qq = 0; qq < LTQ; ++qq) {
                 const int k = lk[qq], m = lm[qq];

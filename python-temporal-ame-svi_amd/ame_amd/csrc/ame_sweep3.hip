@@ -310,6 +310,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     const float* xo = a.x_old + (size_t)tl * n * D;
     float* xn = a.x_new + (size_t)tl * n * D;
     float* cvs = a.cov + (size_t)tl * n * DD;
+    float* cvw = (a.cov_new != nullptr ? a.cov_new : a.cov) + (size_t)tl * n * DD;   // damped output
     const float* ysl = a.Yt + (size_t)tl * n * n * 2;
     const float* xr = (tg < Tt - 1) ? ((tl < TL - 1) ? a.x_old + (size_t)(tl + 1) * n * D : a.next_old)
                                     : nullptr;
@@ -836,7 +837,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 const double* rp = rec + (size_t)ppar * D * 8;
                 const double* pdp = pdl + (size_t)ppar * D;
                 const float* co = cring + (size_t)((i + 3) & 3) * LY::cs;   // node i-1
-                float* cv = cvs + (size_t)(i > 0 ? i - 1 : 0) * DD;
+                float* cv = cvw + (size_t)(i > 0 ? i - 1 : 0) * DD;
 #pragma unroll
                 for (int q = 0; q < LTQ; ++q) {
                     const bool ok = lk[q] >= 0;

@@ -4,8 +4,8 @@ One engine per process / GPU.  It owns, for the local time slices
 [t_begin, t_begin + T_local):
 
     Yt        [T_local][n][n][2] fp32   observed network, time-major (ame_pack_y)
-    x_a, x_b  [T_local][n][d]    fp32   means, ping-pong (old / new of a sweep)
-    cov       [T_local][n][d][d] fp32   covariances, updated in place
+    x_a, x_b  [T_local][n][d]    fp32   means: current state / spare
+    cov, cov_b[T_local][n][d][d] fp32   covariances: current state / spare
     hand      [T_local][n][d]    u64    lane-to-lane {epoch,value} granules
     cov_terms [T_local][n][4]    fp64   per-(node,time) covariance ELBO terms
 
@@ -17,11 +17,22 @@ and runs, per fit() iteration (reference base.py:170-181):
 
 The host then assembles ELBO and MSE from 8 fp64 sums (+ the analytic
 constants) exactly as the reference's formulas define them.
+
+A sweep reads the current state and writes the spare buffers, which become
+current when the sweep is committed.  While fit() has another iteration to
+go, the next sweep does not depend on this iteration's ELBO, so it is started
+on a high-priority stream of its own before this iteration's ELBO kernels,
+which then run beside it on the main stream (they read only the current
+state); the next update_step merely commits it.  When fit() stops instead
+(convergence or max_iter) the started sweep is dropped: it never touched the
+current state.  Results are bit-identical to running the kernels in order
+(tests/test_gpu_parity.py::test_speculative_sweep_is_exact).
 """
 from __future__ import annotations
 
 import ctypes
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -141,6 +152,7 @@ class DeviceEngine:
             self.x_a = X_mean[:, t0:t1].detach().float().permute(1, 0, 2).contiguous().to(dev)
             self.x_b = torch.empty_like(self.x_a)
             self.cov = X_cov[:, t0:t1].detach().float().permute(1, 0, 2, 3).contiguous().to(dev)
+            self.cov_b = torch.empty_like(self.cov)
             n, d, TL = self.n, self.d, sh.T_local
             self.hand = torch.zeros(TL * n * d, dtype=torch.int64, device=dev)
             self.cov_terms = torch.zeros(TL * n * 4, dtype=torch.float64, device=dev)
@@ -164,23 +176,27 @@ class DeviceEngine:
         self._out_valid = False
         self.timing = False       # record HIP events around each kernel launch
         self.events = []          # (name, start, end) while timing
+        self.speculation = os.environ.get("AME_SPECULATE", "1") != "0"
+        self._spec = None         # done-event of a sweep started ahead of its update_step
+        self.sweep_stream = torch.cuda.Stream(device=self.dev, priority=-1)
 
     # ------------------------------------------------------------------
     def _sp(self):
         return ctypes.c_void_p(self.stream.cuda_stream)
 
-    def _tic(self, name):
+    def _tic(self, name, stream=None):
         if not self.timing:
             return None
+        s = self.stream if stream is None else stream
         e = torch.cuda.Event(enable_timing=True)
-        e.record(self.stream)
-        return (name, e)
+        e.record(s)
+        return (name, e, s)
 
     def _toc(self, tok):
         if tok is None:
             return
         e = torch.cuda.Event(enable_timing=True)
-        e.record(self.stream)
+        e.record(tok[2])
         self.events.append((tok[0], tok[1], e))
 
     def kernel_ms(self):
@@ -208,29 +224,60 @@ class DeviceEngine:
         del src
 
     # ------------------------------------------------------------------
-    def sweep(self):
-        """One Gauss-Seidel sweep + covariance update (reference _update_step)."""
-        sh = self.shard
+    def _launch_sweep(self, stream):
+        """Enqueue one sweep (x_a, cov) -> (x_b, cov_b) on `stream`."""
         self.epoch += 1
         halo_in = halo_out = next_old = None
         if self.halo is not None:
             next_old, halo_in, halo_out = self.halo.before_sweep(self)
+        if stream is not self.stream:   # after everything already queued on the main stream
+            ready = torch.cuda.Event()
+            ready.record(self.stream)
+            stream.wait_event(ready)
         a = _lib.ame_sweep_args(
             Yt=_ptr(self.Yt), x_old=_ptr(self.x_a), x_new=_ptr(self.x_b), next_old=next_old,
             hand=_ptr(self.hand), halo_in=halo_in, halo_out=halo_out, cov=_ptr(self.cov),
             consts=_ptr(self.consts), rinv=self.C.rinv4(), lr=self.lr,
             one_minus_lr=float(1.0 - self.lr), epoch=self.epoch, status=_ptr(self.status),
-            work=_ptr(self.sweep_work))
-        tok = self._tic("sweep")
-        _lib.check(self.L.ame_sweep(ctypes.byref(self.dims), ctypes.byref(a), self._sp()),
-                   "ame_sweep")
+            work=_ptr(self.sweep_work), cov_new=_ptr(self.cov_b))
+        tok = self._tic("sweep", stream)
+        _lib.check(self.L.ame_sweep(ctypes.byref(self.dims), ctypes.byref(a),
+                                    ctypes.c_void_p(stream.cuda_stream)), "ame_sweep")
         self._toc(tok)
+
+    def _swap(self):
         self.x_a, self.x_b = self.x_b, self.x_a
-        self.refresh_cov_terms()
+        self.cov, self.cov_b = self.cov_b, self.cov
         self._out_valid = False
-        self._cov_terms_valid = True
+        self._cov_terms_valid = False
+
+    def sweep(self):
+        """One Gauss-Seidel sweep + covariance update (reference _update_step).
+        A sweep already started from this state (speculate) is only committed."""
+        if self._spec is not None:
+            done, self._spec = self._spec, None
+            self.stream.wait_event(done)
+        else:
+            self._launch_sweep(self.stream)
+        self._swap()
         if self.halo is not None:
             self.halo.after_sweep(self)
+
+    def speculate(self):
+        """Start the next sweep now, from the current state, on the sweep stream."""
+        if self._spec is not None or not self.speculation:
+            return
+        self._launch_sweep(self.sweep_stream)
+        done = torch.cuda.Event()
+        done.record(self.sweep_stream)
+        self._spec = done
+
+    def discard_speculation(self):
+        """Drop a started sweep that will not be committed.  It writes only the
+        spare buffers; later main-stream work is ordered after it."""
+        if self._spec is not None:
+            self.stream.wait_event(self._spec)
+            self._spec = None
 
     def refresh_cov_terms(self):
         """Covariance ELBO terms of the current covariances (no update)."""
@@ -257,9 +304,12 @@ class DeviceEngine:
                    "ame_elbo")
         self._toc(tok)
 
-    def sums(self):
-        """The 8 fp64 sums for the current state (all ranks reduced)."""
+    def sums(self, speculate=False):
+        """The 8 fp64 sums for the current state (all ranks reduced).  With
+        speculate=True the next sweep is started first and runs beside them."""
         if not self._out_valid:
+            if speculate:
+                self.speculate()
             self.launch_elbo()
             out = self.out
             if self.halo is not None:
@@ -269,8 +319,8 @@ class DeviceEngine:
             self._out_valid = True
         return self._out_host
 
-    def terms(self):
-        return assemble(self.sums(), self.n, self.T, self.d, self.variant, self.C)
+    def terms(self, speculate=False):
+        return assemble(self.sums(speculate), self.n, self.T, self.d, self.variant, self.C)
 
     def _check_status(self):
         st = int(self.status.item())
@@ -293,12 +343,14 @@ class DeviceEngine:
         return self.cov.permute(1, 0, 2, 3)
 
     def set_means(self, X_mean: torch.Tensor):
+        self.discard_speculation()
         sh = self.shard
         t0, t1 = sh.t_begin, sh.t_begin + sh.T_local
         self.x_a.copy_(X_mean[:, t0:t1].detach().float().permute(1, 0, 2))
         self.invalidate()
 
     def set_covs(self, X_cov: torch.Tensor):
+        self.discard_speculation()
         sh = self.shard
         t0, t1 = sh.t_begin, sh.t_begin + sh.T_local
         self.cov.copy_(X_cov[:, t0:t1].detach().float().permute(1, 0, 2, 3))

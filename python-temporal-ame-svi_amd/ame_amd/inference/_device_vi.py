@@ -122,8 +122,18 @@ class DeviceTemporalVI(BaseTemporalVariationalInference):
         self._stale["mean"] = True
         self._stale["cov"] = True
 
+    # ---------------- fit() hooks: the speculation window ----------------
+    def _fit_iteration(self, iteration: int, max_iter: int) -> None:
+        # another iteration follows this one unless fit() converges first
+        self._spec_next = iteration < max_iter - 1
+
+    def _fit_end(self) -> None:
+        self._spec_next = False
+        if self._engine is not None:
+            self._engine.discard_speculation()
+
     def _terms(self):
-        return self._ensure_engine().terms()
+        return self._ensure_engine().terms(speculate=getattr(self, "_spec_next", False))
 
     def _compute_elbo(self):
         # the reference returns a 0-d fp32 tensor (python float + fp32 tensors)

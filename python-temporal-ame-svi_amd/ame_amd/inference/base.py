@@ -46,30 +46,40 @@ class BaseVariationalInference(ABC):
         converged = False
         patience_counter = 0
         prev_elbo = -np.inf
-        for iteration in range(max_iter):
-            self._update_step()
-            elbo = self._compute_elbo()
-            self.history["elbo"].append(elbo)
-            recon_error = self._compute_reconstruction_error()
-            self.history["reconstruction_error"].append(recon_error)
-            if iteration > 0:
-                rel_change = abs(elbo - prev_elbo) / (abs(prev_elbo) + 1e-8)
-                if rel_change < tolerance:
-                    patience_counter += 1
-                else:
-                    patience_counter = 0
-                if patience_counter >= 3:
-                    converged = True
-            prev_elbo = elbo
-            if verbose and (iteration % check_every == 0 or iteration == max_iter - 1):
-                self._print_progress(iteration, elbo, recon_error)
-            if converged:
-                if verbose:
-                    print(f"\nConverged at iteration {iteration}")
-                break
+        try:
+            for iteration in range(max_iter):
+                self._fit_iteration(iteration, max_iter)
+                self._update_step()
+                elbo = self._compute_elbo()
+                self.history["elbo"].append(elbo)
+                recon_error = self._compute_reconstruction_error()
+                self.history["reconstruction_error"].append(recon_error)
+                if iteration > 0:
+                    rel_change = abs(elbo - prev_elbo) / (abs(prev_elbo) + 1e-8)
+                    if rel_change < tolerance:
+                        patience_counter += 1
+                    else:
+                        patience_counter = 0
+                    if patience_counter >= 3:
+                        converged = True
+                prev_elbo = elbo
+                if verbose and (iteration % check_every == 0 or iteration == max_iter - 1):
+                    self._print_progress(iteration, elbo, recon_error)
+                if converged:
+                    if verbose:
+                        print(f"\nConverged at iteration {iteration}")
+                    break
+        finally:
+            self._fit_end()
         if verbose and not converged:
             print("\nReached maximum iterations without convergence")
         return self.history
+
+    def _fit_iteration(self, iteration: int, max_iter: int) -> None:
+        """Hook: fit() is about to run `iteration` of `max_iter` (no-op here)."""
+
+    def _fit_end(self) -> None:
+        """Hook: fit() is returning or raising (no-op here)."""
 
     def _compute_reconstruction_error(self) -> float:
         if hasattr(self, "get_variational_means"):

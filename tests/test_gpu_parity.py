@@ -121,7 +121,8 @@ def test_single_node_update(gpu_device):
 @pytest.mark.parametrize("n,T,r,method,lr", [
     (33, 7, 1, "good", 0.5), (64, 16, 4, "good", 0.01), (50, 9, 5, "bad", 1.0),
     (48, 6, 8, "naive", 0.3), (70, 5, 6, "good", 1.0), (40, 4, 16, "good", 0.01),
-    (20, 1, 2, "good", 1.0), (2, 3, 2, "bad", 0.7), (24, 3, 7, "naive", 1.0)])
+    (20, 1, 2, "good", 1.0), (2, 3, 2, "bad", 0.7), (24, 3, 7, "naive", 1.0),
+    (1000, 2, 16, "good", 0.5), (700, 3, 8, "naive", 1.0), (900, 2, 16, "bad", 0.2)])
 def test_vs_oracle_fp64(n, T, r, method, lr, gpu_device):
     """Random configurations (odd r, T=1, n=2, ...) against the fp64 oracle.
 
@@ -189,3 +190,44 @@ def test_deterministic(gpu_device):
     assert np.array_equal(outs[0][0], outs[1][0])
     assert np.array_equal(outs[0][1], outs[1][1])
     assert outs[0][2] == outs[1][2] and outs[0][3] == outs[1][3]
+
+
+def _twins(n, T, r, method, lr, dev):
+    """Two identical runs: the engine's speculative schedule and the in-order one."""
+    from ame_amd import TemporalAMEModel
+    out = []
+    for spec in (True, False):
+        m = TemporalAMEModel(n, T, r, seed=3)
+        m.generate_data_fast(seed=4)
+        vi = _vi(m, method, lr, dev)
+        vi.engine.speculation = spec
+        out.append(vi)
+    return out
+
+
+def test_speculative_sweep_is_exact(gpu_device):
+    """The next sweep started beside the ELBO kernels: bit-identical states and
+    histories to running every kernel in order."""
+    a, b = _twins(80, 9, 4, "good", 0.3, gpu_device)
+    ha = a.fit(max_iter=5, tolerance=0.0, verbose=False)
+    hb = b.fit(max_iter=5, tolerance=0.0, verbose=False)
+    assert np.array_equal(a.X_mean.numpy(), b.X_mean.numpy())
+    assert np.array_equal(a.X_cov.numpy(), b.X_cov.numpy())
+    assert [float(e) for e in ha["elbo"]] == [float(e) for e in hb["elbo"]]
+    assert ha["reconstruction_error"] == hb["reconstruction_error"]
+
+
+def test_speculation_dropped_on_convergence(gpu_device):
+    """fit() stops at convergence: the started sweep leaves no trace, and a later
+    fit() continues exactly like the in-order run."""
+    a, b = _twins(60, 7, 3, "naive", 0.5, gpu_device)
+    for vi in (a, b):
+        vi.fit(max_iter=10, tolerance=1.0, verbose=False)   # converges at iteration 3
+    assert len(a.history["elbo"]) == len(b.history["elbo"]) == 4
+    assert np.array_equal(a.X_mean.numpy(), b.X_mean.numpy())
+    assert np.array_equal(a.X_cov.numpy(), b.X_cov.numpy())
+    for vi in (a, b):
+        vi.fit(max_iter=2, tolerance=0.0, verbose=False)
+    assert np.array_equal(a.X_mean.numpy(), b.X_mean.numpy())
+    assert np.array_equal(a.X_cov.numpy(), b.X_cov.numpy())
+    assert [float(e) for e in a.history["elbo"]] == [float(e) for e in b.history["elbo"]]
