@@ -86,6 +86,12 @@ typedef struct ame_sweep_args {
     float* cov_new;              /* [T_local][n][d][d] damped covariances after the sweep, or NULL
                                     (in place).  A separate buffer lets ame_cov / ame_elbo read
                                     `cov` while the next sweep already runs (engine speculation) */
+    uint32_t* done;              /* [T_local] per-slice "finished sweep <epoch>" words (zeroed once by
+                                    the caller), or NULL */
+    uint32_t wait_epoch;         /* 0, or: slice t starts only once done[t] and done[t+1] reach this
+                                    epoch, so the next sweep can be queued while the previous one
+                                    (epoch wait_epoch) still runs.  Needs ame_sweep_orders_slices()
+                                    and room for both sweeps' workgroups (2 T_local <= max_slices) */
 } ame_sweep_args;
 
 typedef struct ame_cov_args {
@@ -119,6 +125,9 @@ int ame_pack_y(const float* Y, float* Yt, const ame_dims* dims,
  * reference node order exactly: step (i,t) sees new means of nodes j<i at t
  * and of node i at t-1, and old means of nodes j>i at t and of node i at t+1. */
 int ame_sweep(const ame_dims* dims, const ame_sweep_args* args, void* stream);
+
+/* 1 when ame_sweep for (n, r) honours done / wait_epoch, else 0. */
+int ame_sweep_orders_slices(int n, int r);
 
 /* Scratch doubles ame_sweep needs in args->work. */
 long long ame_sweep_work_size(const ame_dims* dims);

@@ -31,7 +31,8 @@ class ame_sweep_args(ctypes.Structure):
                 ("hand", c_vp), ("halo_in", c_vp), ("halo_out", c_vp), ("cov", c_vp),
                 ("consts", c_vp), ("rinv", ctypes.c_double * 4), ("lr", ctypes.c_float),
                 ("one_minus_lr", ctypes.c_float), ("epoch", ctypes.c_uint32), ("status", c_vp),
-                ("work", c_vp), ("cov_new", c_vp)]
+                ("work", c_vp), ("cov_new", c_vp), ("done", c_vp),
+                ("wait_epoch", ctypes.c_uint32)]
 
 
 class ame_cov_args(ctypes.Structure):
@@ -45,7 +46,7 @@ class ame_elbo_args(ctypes.Structure):
 
 
 # every symbol include/ame_amd.h declares (checked by tests/test_capi.py)
-EXPORTS = ("ame_pack_y", "ame_sweep", "ame_sweep_work_size", "ame_sweep_max_slices", "ame_sweep_lds_bytes", "ame_cov",
+EXPORTS = ("ame_pack_y", "ame_sweep", "ame_sweep_work_size", "ame_sweep_orders_slices", "ame_sweep_max_slices", "ame_sweep_lds_bytes", "ame_cov",
            "ame_elbo", "ame_elbo_work_size", "ame_host_register", "ame_host_unregister",
            "ame_supported_r", "ame_last_error", "ame_version")
 
@@ -66,6 +67,8 @@ def _declare(L):
     L.ame_elbo_work_size.restype = ctypes.c_longlong
     L.ame_debug_selftest.argtypes = [c_vp, c_vp]
     L.ame_debug_selftest.restype = ctypes.c_int
+    L.ame_sweep_orders_slices.argtypes = [ctypes.c_int, ctypes.c_int]
+    L.ame_sweep_orders_slices.restype = ctypes.c_int
     L.ame_sweep_work_size.argtypes = [P(ame_dims)]
     L.ame_sweep_work_size.restype = ctypes.c_longlong
     L.ame_supported_r.argtypes = [P(ctypes.c_int), ctypes.c_int]

@@ -115,6 +115,8 @@ int ame_sweep_max_slices(int n, int r) {
     return per_cu * cus;
 }
 
+int ame_sweep_orders_slices(int n, int r) { return r_supported(r) && use_v3(n, r) ? 1 : 0; }
+
 long long ame_sweep_work_size(const ame_dims* dims) {
     if (check_dims(dims)) return -1;
     return ame_sweep3_work_doubles(dims);
@@ -139,7 +141,8 @@ int ame_sweep(const ame_dims* dims, const ame_sweep_args* a, void* stream) {
     const bool v3 = use_v3(dims->n, dims->r);
     if (!v3 && sweep_lds_layout(dims->n, dims->r).total > 163840)
         return fail("ame_sweep: slice state (n=%d, r=%d) exceeds one workgroup's LDS", dims->n, dims->r);
-    if (v3 && !a->work) return fail("ame_sweep: work is NULL");
+    if (a->wait_epoch != 0 && (!v3 || !a->done))
+        return fail("ame_sweep: wait_epoch needs the v3 sweep and a done array");
     const int maxs = ame_sweep_max_slices(dims->n, dims->r);
     if (dims->T_local > maxs)
         return fail("ame_sweep: T_local=%d exceeds co-resident workgroups (%d)", dims->T_local, maxs);

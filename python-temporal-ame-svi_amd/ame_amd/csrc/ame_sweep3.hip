@@ -33,7 +33,14 @@
 //           rows, old covariances, old means and the hand-off granules, so no
 //           wave holds prefetch registers.
 //  * one workgroup barrier per step; intra-step hand-offs through LDS
-//    counters.
+//    counters;
+//  * the slice's base inverse P_0^-1 is formed in the prologue (fp64 sums over
+//    the slice's old means + symmetric sweep operator), so a slice can start
+//    as soon as its own inputs exist: with wait_epoch set, the workgroup of
+//    slice t first waits until the previous sweep has finished slices t and
+//    t+1 (per-slice done flags, agent-scope release / acquire).  The next sweep
+//    is then queued while this one runs, and consecutive sweeps overlap instead
+//    of each paying the wavefront fill.
 #include "ame_common.h"
 #include "ame_wave.h"
 
@@ -314,8 +321,6 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     const float* ysl = a.Yt + (size_t)tl * n * n * 2;
     const float* xr = (tg < Tt - 1) ? ((tl < TL - 1) ? a.x_old + (size_t)(tl + 1) * n * D : a.next_old)
                                     : nullptr;
-    const double* K0 = a.work + (size_t)tl * DD;
-    const double* ssq0 = a.work + (size_t)TL * DD + (size_t)tl * M2;
     const double* QiPhi = a.consts + 3 * (size_t)DD;
     bool dead = false;
 
@@ -398,7 +403,125 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     }
 #endif
     // ============================ prologue ============================
-    for (int e = tid; e < DD; e += kNT) Kbuf[e] = K0[e];
+    // pipelined launch: the previous sweep must have finished slices t and t+1
+    // (their means and covariances are this sweep's inputs; slice t+1 also reads
+    // this slice's hand-off granules, which this sweep overwrites)
+    if (a.wait_epoch != 0u) {
+        if (tid == 0) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            for (int q = 0; q < 2 && tl + q < TL; ++q) {
+                while (__hip_atomic_load(a.done + tl + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                       a.wait_epoch) {
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > AME_SPIN_TICKS_LOCAL) {
+                        atomicOr(a.status, AME_STATUS_SPIN_TIMEOUT);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(8);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+    }
+    // P_0 = Pconst + sum_{j>=1} F_j(old), F_j = J_j^T R^-1 J_j (fp64), and its
+    // inverse -> Kbuf[0] by the in-place symmetric sweep operator; naive variant:
+    // column sums of squares of (U, V) over all nodes -> red[]
+    {
+        constexpr int EQ = (NLT + kNT - 1) / kNT;
+        float* st = (float*)yring;   // staging: CH nodes x 2r (the rings are not live yet)
+        double* piv = vbuf;
+        double* K = Kbuf;
+        const int CH = min(64, (8 * YS) / M2);
+        const double pp = r00, ss = r11, qq = 0.5 * (r01 + r10);
+        double acc[EQ];
+        int ek[EQ], em[EQ];
+#pragma unroll
+        for (int u = 0; u < EQ; ++u) {
+            acc[u] = 0.0;
+            const int e = tid + kNT * u;
+            int k = -1, m = -1;
+            if (e < NLT) tri_decode3(e, k, m);
+            ek[u] = k;
+            em[u] = m;
+        }
+        double sq = 0.0;
+        for (int j0 = 1; j0 < n; j0 += CH) {
+            const int cnt = min(CH, n - j0);
+            __syncthreads();
+            for (int e = tid; e < cnt * M2; e += kNT) {
+                const int jj = e / M2, c = e - jj * M2;
+                st[e] = xo[(size_t)(j0 + jj) * D + 2 + c];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < EQ; ++u) {
+                const int k = ek[u], m = em[u];
+                if (k < 2) continue;
+                const int ck = k - 2;
+                const int kc = (ck < R) ? R + ck : ck - R;   // row U_ck pairs with V, row V with U
+                double a0 = 0.0;
+                if (m < 2) {
+                    for (int jj = 0; jj < cnt; ++jj) a0 += (double)st[jj * M2 + kc];
+                } else {
+                    const int cm = m - 2;
+                    const int mc = (cm < R) ? R + cm : cm - R;
+                    for (int jj = 0; jj < cnt; ++jj)
+                        a0 = fma((double)st[jj * M2 + kc], (double)st[jj * M2 + mc], a0);
+                }
+                acc[u] += a0;
+            }
+            if (tid < M2)
+                for (int jj = 0; jj < cnt; ++jj) {
+                    const double v = (double)st[jj * M2 + tid];
+                    sq = fma(v, v, sq);
+                }
+        }
+        if (tid < M2) {   // node 0 joins the sums of squares
+            const double v = (double)xo[2 + tid];
+            red[tid] = fma(v, v, sq);
+        }
+#pragma unroll
+        for (int u = 0; u < EQ; ++u) {
+            const int k = ek[u], m = em[u];
+            if (k < 0) continue;
+            double v;
+            if (k < 2) {
+                v = ((k == 0 && m == 0) ? pp : (k == 1 && m == 1) ? ss : qq) * (double)(n - 1);
+            } else {
+                const bool ku = (k - 2) < R;
+                if (m < 2) {
+                    v = (ku ? (m == 0 ? pp : qq) : (m == 0 ? qq : ss)) * acc[u];
+                } else {
+                    const bool mu_ = (m - 2) < R;
+                    v = ((ku && mu_) ? pp : ((!ku && !mu_) ? ss : qq)) * acc[u];
+                }
+            }
+            v += pconst_entry(a.consts, D, k, m, tg, Tt);
+            K[k * D + m] = v;
+            K[m * D + k] = v;
+        }
+        __syncthreads();
+        for (int pv = 0; pv < D; ++pv) {   // K -> -P_0^-1
+            if (tid < D) piv[tid] = K[pv * D + tid];
+            __syncthreads();
+            const double rinv = 1.0 / piv[pv];
+            for (int e = tid; e < NLT; e += kNT) {
+                int k, m;
+                tri_decode3(e, k, m);
+                double v;
+                if (k == pv && m == pv) v = -rinv;
+                else if (k == pv) v = piv[m] * rinv;
+                else if (m == pv) v = piv[k] * rinv;
+                else v = K[k * D + m] - (piv[k] * piv[m]) * rinv;
+                K[k * D + m] = v;
+                K[m * D + k] = v;
+            }
+            __syncthreads();
+        }
+        for (int e = tid; e < DD; e += kNT) K[e] = -K[e];
+        __syncthreads();
+    }
     for (int e = tid; e < 2 * D * MCP; e += kNT) {   // QiPhi, PhiTQi (adjacent in consts), padded
         const int mat = e / (D * MCP), rc = e - mat * D * MCP, rr = rc / MCP, cc = rc - rr * MCP;
         arQ[e] = (cc < D) ? QiPhi[(size_t)mat * DD + rr * D + cc] : 0.0;
@@ -441,7 +564,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         }
     }
     double ssq_l = 0.0;   // solver, naive: running sum of squares of column `lane`
-    if (tid < D && is_naive && tid >= 2) ssq_l = ssq0[tid - 2];
+    if (tid < D && is_naive && tid >= 2) ssq_l = red[tid - 2];
     if (wave == 7) {   // rings read by steps 0..2 and the prologue
         for (int q = 0; q < 5; ++q) dma_x(q);
         for (int q = 0; q < 4; ++q) dma_r(q);
@@ -932,119 +1055,17 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             lds_barrier3();
         }
     }
-}
-
-// ---------------------------------------------------------------------------
-// prep: per slice P_0 = Pconst + sum_{j >= 1} F_j(old) in fp64, its inverse
-// K_0 (in-place symmetric sweep operator), and the naive variant's column sums
-// of squares.  One 256-thread workgroup per slice.
-// ---------------------------------------------------------------------------
-template <int R>
-__global__ void __launch_bounds__(AME_NT)
-ame_sweep3_prep_kernel(ame_dims dm, const float* __restrict__ x_old, const double* __restrict__ consts,
-                       double r00, double r01, double r10, double r11, double* __restrict__ work) {
-    constexpr int D = 2 + 2 * R, M2 = 2 * R, NLT = D * (D + 1) / 2, DD = D * D;
-    constexpr int CH = 64;   // nodes staged per chunk
-    const int n = dm.n, TL = dm.T_local, Tt = dm.T_total;
-    const int tl = blockIdx.x, tg = dm.t_begin + tl;
-    const int tid = threadIdx.x;
-    __shared__ float st[CH * M2];
-    __shared__ double K[DD];
-    __shared__ double piv[D];
-    const float* xs = x_old + (size_t)tl * n * D;
-    const double p = r00, s = r11, q = 0.5 * (r01 + r10);
-    constexpr int EQ = (NLT + AME_NT - 1) / AME_NT;
-    double acc[EQ];
-    int ek[EQ], em[EQ];
-#pragma unroll
-    for (int u = 0; u < EQ; ++u) {
-        acc[u] = 0.0;
-        const int e = tid + AME_NT * u;
-        int k = -1, m = -1;
-        if (e < NLT) tri_decode3(e, k, m);
-        ek[u] = k;
-        em[u] = m;
-    }
-    double sq = 0.0;   // thread tid < M2: sum over all nodes of column tid squared
-    for (int j0 = 1; j0 < n; j0 += CH) {   // nodes j >= 1
-        const int cnt = min(CH, n - j0);
+    // ---- slice done: release its means, covariances and granules, then flag it
+    // for the next sweep (every wave drains its own stores first) ----
+    if (a.done != nullptr) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        for (int e = tid; e < cnt * M2; e += AME_NT) {
-            const int jj = e / M2, c = e - jj * M2;
-            st[e] = xs[(size_t)(j0 + jj) * D + 2 + c];
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(a.done + tl, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < EQ; ++u) {
-            const int k = ek[u], m = em[u];
-            if (k < 2) continue;
-            const int ck = k - 2;
-            const bool ku = ck < R;                      // row U_ck: J entry V ; row V: J entry U
-            const int kc = ku ? R + ck : ck - R;
-            if (m < 2) {
-                double a0 = 0.0;
-                for (int jj = 0; jj < cnt; ++jj) a0 += (double)st[jj * M2 + kc];
-                acc[u] += a0;
-            } else {
-                const int cm = m - 2;
-                const int mc = (cm < R) ? R + cm : cm - R;
-                double a0 = 0.0;
-                for (int jj = 0; jj < cnt; ++jj)
-                    a0 = fma((double)st[jj * M2 + kc], (double)st[jj * M2 + mc], a0);
-                acc[u] += a0;
-            }
-        }
-        if (tid < M2)
-            for (int jj = 0; jj < cnt; ++jj) {
-                const double v = (double)st[jj * M2 + tid];
-                sq = fma(v, v, sq);
-            }
     }
-    if (tid < M2) {   // add node 0 to the sums of squares
-        const double v = (double)xs[2 + tid];
-        work[(size_t)TL * DD + (size_t)tl * M2 + tid] = fma(v, v, sq);
-    }
-#pragma unroll
-    for (int u = 0; u < EQ; ++u) {
-        const int k = ek[u], m = em[u];
-        if (k < 0) continue;
-        double v;
-        if (k < 2) {
-            v = ((k == 0 && m == 0) ? p : (k == 1 && m == 1) ? s : q) * (double)(n - 1);
-        } else {
-            const int ck = k - 2;
-            const bool ku = ck < R;
-            if (m < 2) {
-                v = (ku ? (m == 0 ? p : q) : (m == 0 ? q : s)) * acc[u];
-            } else {
-                const bool mu_ = (m - 2) < R;
-                v = ((ku && mu_) ? p : ((!ku && !mu_) ? s : q)) * acc[u];
-            }
-        }
-        v += pconst_entry(consts, D, k, m, tg, Tt);
-        K[k * D + m] = v;
-        K[m * D + k] = v;
-    }
-    __syncthreads();
-    for (int pv = 0; pv < D; ++pv) {   // in-place symmetric sweep: K -> -P_0^-1
-        if (tid < D) piv[tid] = K[pv * D + tid];
-        __syncthreads();
-        const double rinv = 1.0 / piv[pv];
-        for (int e = tid; e < NLT; e += AME_NT) {
-            int k, m;
-            tri_decode3(e, k, m);
-            double v;
-            if (k == pv && m == pv) v = -rinv;
-            else if (k == pv) v = piv[m] * rinv;
-            else if (m == pv) v = piv[k] * rinv;
-            else v = K[k * D + m] - (piv[k] * piv[m]) * rinv;
-            K[k * D + m] = v;
-            K[m * D + k] = v;
-        }
-        __syncthreads();
-    }
-    double* K0 = work + (size_t)tl * DD;
-    for (int e = tid; e < DD; e += AME_NT) K0[e] = -K[e];
 }
 
 
@@ -1098,9 +1119,6 @@ int ame_sweep3_supported(int n, int r) {
 template <int R>
 static int launch_sweep3(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {
     const int lds = l3_total<R>(dm->n);
-    hipLaunchKernelGGL(ame_sweep3_prep_kernel<R>, dim3(dm->T_local), dim3(AME_NT), 0, st, *dm, a->x_old,
-                       a->consts, a->rinv[0], a->rinv[1], a->rinv[2], a->rinv[3], a->work);
-    if (hipGetLastError() != hipSuccess) return -3;
     auto kern = ame_sweep3_kernel<R>;
     if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
         hipSuccess)
@@ -1120,6 +1138,6 @@ int ame_sweep3_dispatch(const ame_dims* dm, const ame_sweep_args* a, hipStream_t
 }
 
 long long ame_sweep3_work_doubles(const ame_dims* dm) {
-    const long long D = 2 + 2LL * dm->r;
-    return (long long)dm->T_local * (D * D + 2LL * dm->r);
+    (void)dm;   // the base inverse lives in LDS (formed in the sweep prologue)
+    return 0;
 }

@@ -25,8 +25,12 @@ on a high-priority stream of its own before this iteration's ELBO kernels,
 which then run beside it on the main stream (they read only the current
 state); the next update_step merely commits it.  When fit() stops instead
 (convergence or max_iter) the started sweep is dropped: it never touched the
-current state.  Results are bit-identical to running the kernels in order
-(tests/test_gpu_parity.py::test_speculative_sweep_is_exact).
+current state.  On one GPU, when both sweeps' workgroups fit on the chip,
+the next sweep is queued while the previous one still runs (pipelined): each
+of its slices waits on the device for the previous sweep to finish slices t
+and t+1, so consecutive sweeps overlap and the wavefront fill is paid once per
+fit() instead of once per iteration.  Results are bit-identical to running
+the kernels in order (tests/test_gpu_parity.py::test_speculative_sweep_is_exact).
 """
 from __future__ import annotations
 
@@ -178,7 +182,12 @@ class DeviceEngine:
         self.events = []          # (name, start, end) while timing
         self.speculation = os.environ.get("AME_SPECULATE", "1") != "0"
         self._spec = None         # done-event of a sweep started ahead of its update_step
-        self.sweep_stream = torch.cuda.Stream(device=self.dev, priority=-1)
+        # consecutive sweeps alternate between two high-priority streams
+        self.sweep_streams = [torch.cuda.Stream(device=self.dev, priority=-1) for _ in range(2)]
+        self.done = torch.zeros(max(sh.T_local, 1), dtype=torch.int32, device=self.dev)
+        self.pipelined = (bool(self.L.ame_sweep_orders_slices(self.n, self.r))
+                          and self.halo is None and 2 * sh.T_local <= self.max_slices
+                          and os.environ.get("AME_PIPELINE", "1") != "0")
 
     # ------------------------------------------------------------------
     def _sp(self):
@@ -224,13 +233,20 @@ class DeviceEngine:
         del src
 
     # ------------------------------------------------------------------
-    def _launch_sweep(self, stream):
-        """Enqueue one sweep (x_a, cov) -> (x_b, cov_b) on `stream`."""
+    def _launch_sweep(self, spec=False):
+        """Enqueue one sweep (x_a, cov) -> (x_b, cov_b); returns its done-event.
+        A speculative sweep in pipelined mode is queued while the previous sweep
+        (epoch - 1) still runs and orders itself slice by slice on the device;
+        any other sweep is ordered after everything queued on the main stream."""
         self.epoch += 1
+        stream = self.sweep_streams[self.epoch & 1]
         halo_in = halo_out = next_old = None
         if self.halo is not None:
             next_old, halo_in, halo_out = self.halo.before_sweep(self)
-        if stream is not self.stream:   # after everything already queued on the main stream
+        wait = 0
+        if spec and self.pipelined and self.speculation:
+            wait = self.epoch - 1
+        else:
             ready = torch.cuda.Event()
             ready.record(self.stream)
             stream.wait_event(ready)
@@ -239,11 +255,15 @@ class DeviceEngine:
             hand=_ptr(self.hand), halo_in=halo_in, halo_out=halo_out, cov=_ptr(self.cov),
             consts=_ptr(self.consts), rinv=self.C.rinv4(), lr=self.lr,
             one_minus_lr=float(1.0 - self.lr), epoch=self.epoch, status=_ptr(self.status),
-            work=_ptr(self.sweep_work), cov_new=_ptr(self.cov_b))
+            work=_ptr(self.sweep_work), cov_new=_ptr(self.cov_b), done=_ptr(self.done),
+            wait_epoch=wait)
         tok = self._tic("sweep", stream)
         _lib.check(self.L.ame_sweep(ctypes.byref(self.dims), ctypes.byref(a),
                                     ctypes.c_void_p(stream.cuda_stream)), "ame_sweep")
         self._toc(tok)
+        done = torch.cuda.Event()
+        done.record(stream)
+        return done
 
     def _swap(self):
         self.x_a, self.x_b = self.x_b, self.x_a
@@ -256,9 +276,9 @@ class DeviceEngine:
         A sweep already started from this state (speculate) is only committed."""
         if self._spec is not None:
             done, self._spec = self._spec, None
-            self.stream.wait_event(done)
         else:
-            self._launch_sweep(self.stream)
+            done = self._launch_sweep()
+        self.stream.wait_event(done)
         self._swap()
         if self.halo is not None:
             self.halo.after_sweep(self)
@@ -267,10 +287,7 @@ class DeviceEngine:
         """Start the next sweep now, from the current state, on the sweep stream."""
         if self._spec is not None or not self.speculation:
             return
-        self._launch_sweep(self.sweep_stream)
-        done = torch.cuda.Event()
-        done.record(self.sweep_stream)
-        self._spec = done
+        self._spec = self._launch_sweep(spec=True)
 
     def discard_speculation(self):
         """Drop a started sweep that will not be committed.  It writes only the

@@ -231,3 +231,15 @@ def test_speculation_dropped_on_convergence(gpu_device):
     assert np.array_equal(a.X_mean.numpy(), b.X_mean.numpy())
     assert np.array_equal(a.X_cov.numpy(), b.X_cov.numpy())
     assert [float(e) for e in a.history["elbo"]] == [float(e) for e in b.history["elbo"]]
+
+
+def test_pipelined_sweeps_many_slices(gpu_device):
+    """100 slices: consecutive sweeps overlap slice by slice (done flags); the
+    result is bit-identical to the in-order schedule."""
+    a, b = _twins(150, 100, 4, "good", 0.5, gpu_device)
+    assert a.engine.pipelined
+    ha = a.fit(max_iter=4, tolerance=0.0, verbose=False)
+    hb = b.fit(max_iter=4, tolerance=0.0, verbose=False)
+    assert np.array_equal(a.X_mean.numpy(), b.X_mean.numpy())
+    assert np.array_equal(a.X_cov.numpy(), b.X_cov.numpy())
+    assert [float(e) for e in ha["elbo"]] == [float(e) for e in hb["elbo"]]
