@@ -54,6 +54,9 @@ enum ame_variant { AME_GOOD = 0, AME_BAD = 1, AME_NAIVE = 2 };
 #define AME_STATUS_HALO_TIMEOUT 2u
 #define AME_STATUS_LDS_TIMEOUT 4u   /* intra-workgroup hand-off timed out (internal error) */
 
+/* float offset of the done word in a back channel of n*d floats */
+#define AME_BACK_DONE_OFFSET(nd) ((((nd) + 63) / 64) * 64)
+
 typedef struct ame_dims {
     int32_t n;        /* nodes */
     int32_t r;        /* latent_dim; d = 2 + 2r */
@@ -92,6 +95,11 @@ typedef struct ame_sweep_args {
                                     epoch, so the next sweep can be queued while the previous one
                                     (epoch wait_epoch) still runs.  Needs ame_sweep_orders_slices()
                                     and room for both sweeps' workgroups (2 T_local <= max_slices) */
+    float* back_out;             /* time-sharded, rank with a left neighbour: host-mapped
+                                    [n*d floats | done word at AME_BACK_DONE_OFFSET] the first slice
+                                    fills with its new means when it finishes, or NULL */
+    const float* back_in;        /* the right neighbour's back_out: in a pipelined launch
+                                    (wait_epoch != 0) it replaces next_old */
 } ame_sweep_args;
 
 typedef struct ame_cov_args {

@@ -32,7 +32,7 @@ class ame_sweep_args(ctypes.Structure):
                 ("consts", c_vp), ("rinv", ctypes.c_double * 4), ("lr", ctypes.c_float),
                 ("one_minus_lr", ctypes.c_float), ("epoch", ctypes.c_uint32), ("status", c_vp),
                 ("work", c_vp), ("cov_new", c_vp), ("done", c_vp),
-                ("wait_epoch", ctypes.c_uint32)]
+                ("wait_epoch", ctypes.c_uint32), ("back_out", c_vp), ("back_in", c_vp)]
 
 
 class ame_cov_args(ctypes.Structure):

@@ -136,7 +136,7 @@ int ame_sweep(const ame_dims* dims, const ame_sweep_args* a, void* stream) {
     if (a->epoch == 0) return fail("ame_sweep: epoch must be >= 1");
     if (dims->t_begin > 0 && !a->halo_in)
         return fail("ame_sweep: t_begin=%d > 0 needs halo_in", dims->t_begin);
-    if (dims->t_begin + dims->T_local < dims->T_total && !a->next_old)
+    if (dims->t_begin + dims->T_local < dims->T_total && !a->next_old && !(a->wait_epoch && a->back_in))
         return fail("ame_sweep: rank does not hold T-1 and next_old is NULL");
     const bool v3 = use_v3(dims->n, dims->r);
     if (!v3 && sweep_lds_layout(dims->n, dims->r).total > 163840)

@@ -207,6 +207,11 @@ __device__ __forceinline__ void dma16_sys(const void* gsrc, uint32_t lds) {
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc0 sc1\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
 }
+__device__ __forceinline__ void dma4_sys(const void* gsrc, uint32_t lds) {   // host-mapped source
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off sc0 sc1\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
+}
 __device__ __forceinline__ void dma4(const void* gsrc, uint32_t lds) {
     uint32_t keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
@@ -319,7 +324,12 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     float* cvs = a.cov + (size_t)tl * n * DD;
     float* cvw = (a.cov_new != nullptr ? a.cov_new : a.cov) + (size_t)tl * n * DD;   // damped output
     const float* ysl = a.Yt + (size_t)tl * n * n * 2;
-    const float* xr = (tg < Tt - 1) ? ((tl < TL - 1) ? a.x_old + (size_t)(tl + 1) * n * D : a.next_old)
+    // old means of slice t+1: the next local slice, or for the last local slice the
+    // right rank's first slice -- next_old (gathered before the sweep), or in a
+    // pipelined launch the back channel that rank fills when its slice finishes
+    const bool back_rd = (a.wait_epoch != 0u) && (tl == TL - 1) && (a.back_in != nullptr);
+    const float* xr = (tg < Tt - 1) ? ((tl < TL - 1) ? a.x_old + (size_t)(tl + 1) * n * D
+                                                     : (back_rd ? a.back_in : a.next_old))
                                     : nullptr;
     const double* QiPhi = a.consts + 3 * (size_t)DD;
     bool dead = false;
@@ -385,7 +395,8 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     };
     auto dma_r = [&](int node) {   // old mean, slice t+1 -> slot node & 3 : 1 instruction
         const float* src = (xr != nullptr && node < n) ? xr + (size_t)node * D : xo;
-        dma4(src + (lane < D ? lane : 0), lds_off(rring + (node & 3) * 64));
+        if (back_rd) dma4_sys(src + (lane < D ? lane : 0), lds_off(rring + (node & 3) * 64));
+        else dma4(src + (lane < D ? lane : 0), lds_off(rring + (node & 3) * 64));
     };
     auto dma_p = [&](int node) {   // granules of mu_{node, t-1} -> slot node & 3 : 1 instruction
         const uint32_t dst = lds_off(pring + (size_t)(node & 3) * 128);
@@ -418,6 +429,18 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                     }
                     __builtin_amdgcn_s_sleep(8);
                 }
+            }
+            if (back_rd) {   // the right rank's first slice of the previous sweep
+                const uint32_t* bd = (const uint32_t*)(a.back_in + AME_BACK_DONE_OFFSET(n * D));
+                while (__hip_atomic_load(const_cast<uint32_t*>(bd), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_SYSTEM) < a.wait_epoch) {
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > AME_SPIN_TICKS_HALO) {
+                        atomicOr(a.status, AME_STATUS_HALO_TIMEOUT);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(8);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1064,6 +1087,22 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __hip_atomic_store(a.done + tl, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    // ---- first slice of a rank with a left neighbour: its new means are that
+    // rank's next_old in the next (pipelined) sweep; system-scope release ----
+    if (tl == 0 && a.back_out != nullptr) {
+        for (int e = tid; e < n * D; e += kNT)
+            a.back_out[e] = __uint_as_float(__hip_atomic_load(
+                const_cast<uint32_t*>((const uint32_t*)(xn + e)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store((uint32_t*)(a.back_out + AME_BACK_DONE_OFFSET(n * D)), a.epoch,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }

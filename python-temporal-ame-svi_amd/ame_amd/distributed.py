@@ -15,7 +15,12 @@ terms of the boundary slices (structured_mf.py:255-264):
   collective sits on the data path; the wavefront simply continues across the
   GPU boundary;
 * after the sweep: all_gather of last-slice means (the transition term of the
-  ELBO at t_begin) and an fp64 all_reduce of the 8 ELBO/MSE sums.
+  ELBO at t_begin) and an fp64 all_reduce of the 8 ELBO/MSE sums;
+* pipelined sweeps (the next sweep queued while this one runs): the right halo
+  cannot come from a collective, so each rank's first slice also writes its
+  final means into a back channel in the same shared buffer when it finishes
+  (system-scope release + done word), and the left rank's last slice of the
+  next sweep waits for that word instead.
 
 ``shard_range`` / ``assemble``-level logic is exercised on CPU by
 tests/test_distributed_cpu.py (gloo, world_size 2).
@@ -120,7 +125,9 @@ class TimeShardHalo:
             return
         tag = [uuid.uuid4().hex[:12] if self.shard.rank == 0 else None]
         dist.broadcast_object_list(tag, src=0, group=self.group)
-        nbytes = max(4096, eng.n * eng.d * 8)
+        nd = eng.n * eng.d
+        self._back_off = nd * 8                                    # after the granules
+        nbytes = max(4096, self._back_off + (((nd + 63) // 64) * 64 + 64) * 4)
         rank, world = self.shard.rank, self.shard.world
         base = f"/dev/shm/ame_halo_{tag[0]}"
         if rank > 0:   # consumer of boundary (rank-1 -> rank) creates it
@@ -144,14 +151,33 @@ class TimeShardHalo:
         return [o.to(t.device) for o in out]
 
     # ---- engine hooks ----
-    def before_sweep(self, eng):
+    def agree(self, eng, flag: bool) -> bool:
+        """True only if every rank passes True."""
+        t = torch.tensor([1 if flag else 0], dtype=torch.int32,
+                         device="cpu" if self._host_coll else eng.dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+        return bool(t.item())
+
+    def back_channels(self, eng):
+        """(back_in, back_out) device addresses: the right boundary's back channel
+        is read by this rank's last slice, the left one written by its first."""
         self._setup(eng)
-        firsts = self._all_gather_slice(eng.x_a[0])
+        back_in = back_out = None
+        if self.right is not None:
+            back_in = ctypes.c_void_p(self.right.dev.value + self._back_off)
+        if self.left is not None:
+            back_out = ctypes.c_void_p(self.left.dev.value + self._back_off)
+        return back_in, back_out
+
+    def before_sweep(self, eng, gather=True):
+        self._setup(eng)
         rank, world = self.shard.rank, self.shard.world
         next_old = None
-        if rank < world - 1:
-            self._next_old = firsts[rank + 1]
-            next_old = ctypes.c_void_p(self._next_old.data_ptr())
+        if gather:
+            firsts = self._all_gather_slice(eng.x_a[0])
+            if rank < world - 1:
+                self._next_old = firsts[rank + 1]
+                next_old = ctypes.c_void_p(self._next_old.data_ptr())
         halo_in = self.left.dev if self.left is not None else None
         halo_out = self.right.dev if self.right is not None else None
         return next_old, halo_in, halo_out

@@ -186,8 +186,10 @@ class DeviceEngine:
         self.sweep_streams = [torch.cuda.Stream(device=self.dev, priority=-1) for _ in range(2)]
         self.done = torch.zeros(max(sh.T_local, 1), dtype=torch.int32, device=self.dev)
         self.pipelined = (bool(self.L.ame_sweep_orders_slices(self.n, self.r))
-                          and self.halo is None and 2 * sh.T_local <= self.max_slices
+                          and 2 * sh.T_local <= self.max_slices
                           and os.environ.get("AME_PIPELINE", "1") != "0")
+        if self.halo is not None:   # every rank must take the same path
+            self.pipelined = self.halo.agree(self, self.pipelined)
 
     # ------------------------------------------------------------------
     def _sp(self):
@@ -240,11 +242,15 @@ class DeviceEngine:
         any other sweep is ordered after everything queued on the main stream."""
         self.epoch += 1
         stream = self.sweep_streams[self.epoch & 1]
-        halo_in = halo_out = next_old = None
+        pipe = spec and self.pipelined and self.speculation
+        halo_in = halo_out = next_old = back_in = back_out = None
         if self.halo is not None:
-            next_old, halo_in, halo_out = self.halo.before_sweep(self)
+            # a pipelined launch takes next_old from the back channel instead of a
+            # collective that would wait for the running sweep
+            next_old, halo_in, halo_out = self.halo.before_sweep(self, gather=not pipe)
+            back_in, back_out = self.halo.back_channels(self)
         wait = 0
-        if spec and self.pipelined and self.speculation:
+        if pipe:
             wait = self.epoch - 1
         else:
             ready = torch.cuda.Event()
@@ -256,7 +262,7 @@ class DeviceEngine:
             consts=_ptr(self.consts), rinv=self.C.rinv4(), lr=self.lr,
             one_minus_lr=float(1.0 - self.lr), epoch=self.epoch, status=_ptr(self.status),
             work=_ptr(self.sweep_work), cov_new=_ptr(self.cov_b), done=_ptr(self.done),
-            wait_epoch=wait)
+            wait_epoch=wait, back_out=back_out, back_in=back_in)
         tok = self._tic("sweep", stream)
         _lib.check(self.L.ame_sweep(ctypes.byref(self.dims), ctypes.byref(a),
                                     ctypes.c_void_p(stream.cuda_stream)), "ame_sweep")
