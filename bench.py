@@ -210,7 +210,11 @@ def main():
             },
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic},
+                         "traffic": traffic,
+                         "note": ("sweep launches are pipelined: a launch starts while the "
+                                  "previous sweep runs and its duration includes that wait; "
+                                  "the sweep is latency-bound (n dependent steps per slice)")
+                         if getattr(eng, "pipelined", False) else None},
             "kernels_ms": kms,
             "iteration_roofline_frac": b_iter / (dt / args.steps) / (world * HBM_PEAK_GBS * 1e9),
             "cpu_baseline": cpu,
