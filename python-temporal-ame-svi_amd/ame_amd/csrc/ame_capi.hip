@@ -101,13 +101,13 @@ int ame_host_unregister(void* host) {
 
 long long ame_sweep_lds_bytes(int n, int r) {
     if (!r_supported(r) || n < 1) return 0;
-    return sweep_lds_layout(n, r).total;
+    return sweep_lds_layout(n, r, ame_sweep_force_global()).total;
 }
 
 int ame_sweep_max_slices(int n, int r) {
     if (!r_supported(r)) return 0;
     const bool v3 = use_v3(n, r);
-    if (!v3 && sweep_lds_layout(n, r).total > 163840) return 0;
+    if (!v3 && sweep_lds_layout(n, r, ame_sweep_force_global()).total > AME_LDS_MAX) return 0;
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
@@ -139,7 +139,7 @@ int ame_sweep(const ame_dims* dims, const ame_sweep_args* a, void* stream) {
     if (dims->t_begin + dims->T_local < dims->T_total && !a->next_old && !(a->wait_epoch && a->back_in))
         return fail("ame_sweep: rank does not hold T-1 and next_old is NULL");
     const bool v3 = use_v3(dims->n, dims->r);
-    if (!v3 && sweep_lds_layout(dims->n, dims->r).total > 163840)
+    if (!v3 && sweep_lds_layout(dims->n, dims->r, ame_sweep_force_global()).total > AME_LDS_MAX)
         return fail("ame_sweep: slice state (n=%d, r=%d) exceeds one workgroup's LDS", dims->n, dims->r);
     if (a->wait_epoch != 0 && (!v3 || !a->done))
         return fail("ame_sweep: wait_epoch needs the v3 sweep and a done array");

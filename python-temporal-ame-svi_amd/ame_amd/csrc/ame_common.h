@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../../include/ame_amd.h"
 
@@ -64,12 +65,18 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* scratch /* 4*
     }
 }
 
-// Dynamic LDS carve-up of the sweep kernel (host and device agree).
+// Dynamic LDS carve-up of the sweep kernel (host and device agree).  The
+// slice's (U,V) block (n x 2R floats) lives in LDS when everything fits one
+// CU's 160 KiB; otherwise (m_global = 1, e.g. n = 4096 or r = 32) the GEMV
+// reads it from the slice's mean buffers in HBM/L2 (new means for nodes already
+// updated this sweep, old ones after), and it takes no LDS.
+#define AME_LDS_MAX 163840LL
 struct SweepLds {
     long long oK, oVec, oUpd, oRed, oScal, oG, oSsq, oF, oPart, oZ, oM, total;
+    int m_global;
 };
 __host__ __device__ inline long long ame_align16(long long x) { return (x + 15) & ~15LL; }
-__host__ __device__ inline SweepLds sweep_lds_layout(int n, int R) {
+__host__ __device__ inline SweepLds sweep_lds_layout(int n, int R, int force_global = 0) {
     const int D = 2 + 2 * R, M2 = 2 * R, KS = D + 1, US = (M2 + 15) / 16;
     const int VEC = (R % 4 == 0) ? 4 : ((R % 2 == 0) ? 2 : 1);
     const int GW = 192 / (M2 / VEC);
@@ -85,13 +92,24 @@ __host__ __device__ inline SweepLds sweep_lds_layout(int n, int R) {
     L.oF = o;    o = ame_align16(o + 4LL * 5 * D);
     L.oPart = o; o = ame_align16(o + 4LL * GW * (M2 + 2));
     L.oZ = o;    o = ame_align16(o + 8LL * n);
-    L.oM = o;    o = ame_align16(o + 4LL * n * M2);
-    L.total = o;
+    L.oM = o;
+    const long long withM = ame_align16(o + 4LL * n * M2);
+    L.m_global = (force_global || withM > AME_LDS_MAX) ? 1 : 0;
+    L.total = L.m_global ? o : withM;
     return L;
 }
 
+// AME_SWEEP_M_GLOBAL=1 puts the v2 sweep's (U,V) block in HBM even when it
+// would fit in LDS (host side; lets the tests cover that mode at small n).
+inline int ame_sweep_force_global() {
+    const char* e = getenv("AME_SWEEP_M_GLOBAL");
+    return (e && e[0] && e[0] != '0') ? 1 : 0;
+}
+
+// Latent dims compiled into the library.  r = 32 (d = 66, BASELINE config 5)
+// runs on the v2 sweep only (two state rows per lane in the solver wave).
 #ifdef AME_ONLY_R   // diagnostic builds: one latent dim only
 #define AME_FOR_EACH_R(X) X(AME_ONLY_R)
 #else
-#define AME_FOR_EACH_R(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(12) X(16) X(24)
+#define AME_FOR_EACH_R(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(12) X(16) X(24) X(32)
 #endif

@@ -83,16 +83,21 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Wave-0 multi-dot: lanes k < D hold p[v]; every lane gets all NV sums.
+// Wave-0 multi-dot: lane L holds p[h][v] of state rows k = L + 64h < D (KH
+// rows per lane; KH = 2 only for D > 64); every lane gets all NV sums.
 // Reduction: lane L sums red[v][part*QD .. +QD) (v = L>>2, part = L&3, QD =
 // ceil(D/4)), then a 4-lane xor reduction.  NV <= 16.
-template <int NV, int D>
-__device__ __forceinline__ void wave_multidot(const double (&pv)[NV], double (&out)[NV],
+template <int NV, int D, int KH>
+__device__ __forceinline__ void wave_multidot(const double (&pv)[KH][NV], double (&out)[NV],
                                               double* red /* 16*D */, double* sums, int lane) {
     constexpr int QD = (D + 3) / 4;
-    if (lane < D) {
 #pragma unroll
-        for (int v = 0; v < NV; ++v) red[v * D + lane] = pv[v];
+    for (int h = 0; h < KH; ++h) {
+        const int k = lane + 64 * h;
+        if (k < D) {
+#pragma unroll
+            for (int v = 0; v < NV; ++v) red[v * D + k] = pv[h][v];
+        }
     }
     wave_lds_sync();
     const int v = lane >> 2, part = lane & 3;
@@ -129,13 +134,21 @@ __device__ __forceinline__ void tri_decode(int e, int& k, int& m) {
     m = e - k * (k + 1) / 2;
 }
 
-template <int R>
+// MG = false: the slice's (U,V) block lives in LDS (M).  MG = true: it is read
+// from the mean buffers (xn for nodes < split, i.e. already updated in this
+// sweep, xo from split on); wave 0 drains its mean stores (vmcnt(0)) before
+// the barrier that precedes the next GEMV, the workgroup-scope release of the
+// AMDGPU memory model (one CU, shared vL1D).
+template <int R, bool MG>
 __global__ void __launch_bounds__(AME_NT)
 ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     constexpr int D = 2 + 2 * R, M2 = 2 * R, KS = D + 1, US = (M2 + 15) / 16;
+    constexpr int KH = (D + 63) / 64;   // state rows per solver lane
     constexpr int VEC = (R % 4 == 0) ? 4 : ((R % 2 == 0) ? 2 : 1);
     constexpr int CW = M2 / VEC, GW = 192 / CW, PW = M2 + 2;
-    constexpr int MC = (D + 3) / 4;
+    constexpr int NPA = (4 * D <= AME_NT) ? 4 : 2;   // AR row parts
+    constexpr int MC = (D + NPA - 1) / NPA;
+    static_assert(D <= 128 && 128 + D <= AME_NT && NPA * D <= AME_NT, "sweep v2: D too large");
     constexpr int NLT = D * (D + 1) / 2, LTQ = (NLT + AME_NT - 1) / AME_NT;
     const int n = dm.n, TL = dm.T_local, Tt = dm.T_total;
     const int tl = blockIdx.x, tg = dm.t_begin + tl;
@@ -143,7 +156,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     const bool is_naive = dm.variant == AME_NAIVE, is_bad = dm.variant == AME_BAD;
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const SweepLds L = sweep_lds_layout(n, R);
+    const SweepLds L = sweep_lds_layout(n, R, MG ? 1 : 0);
     double* K = (double*)(smem + L.oK);          // D x KS
     double* vec = (double*)(smem + L.oVec);      // (5+US) x D  K-matvec results
     double* upd = (double*)(smem + L.oUpd);      // 8 x D       rank-4 update vectors
@@ -160,7 +173,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     float* mu_old_n = mu_prev + 4 * D;           // mu_{i+1,t}^old
     float* part = (float*)(smem + L.oPart);      // GW x PW   GEMV partials
     float2* z = (float2*)(smem + L.oZ);          // n         z row of the next node
-    float* M = (float*)(smem + L.oM);            // n x 2R    (U,V) of the slice
+    float* M = (float*)(smem + L.oM);            // n x 2R    (U,V) of the slice (!MG)
 
     const double p = a.rinv[0], s = a.rinv[3], q = 0.5 * (a.rinv[1] + a.rinv[2]);
     const double r00 = a.rinv[0], r01 = a.rinv[1], r10 = a.rinv[2], r11 = a.rinv[3];
@@ -178,20 +191,27 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     const float* ysl = a.Yt + (size_t)tl * n * n * 2;
     const float lr = a.lr, om = a.one_minus_lr;
     bool dead = false;
+    // (U,V) row of node j: new for j < split (this sweep), old from split on
+    auto mrow = [&](int j, int split) -> const float* {
+        if constexpr (MG) return (j < split ? (const float*)xn : xo) + (size_t)j * D + 2;
+        else return M + j * M2;
+    };
 
     // ------------------------------------------------------------------
     // init: slice state, P_0 = P_const + sum_{j != 0} F_j, K_0 = P_0^-1
     // ------------------------------------------------------------------
-    for (int idx = tid; idx < n * M2; idx += AME_NT) {
-        const int j = idx / M2, c = idx - j * M2;
-        M[idx] = xo[(size_t)j * D + 2 + c];
+    if constexpr (!MG) {
+        for (int idx = tid; idx < n * M2; idx += AME_NT) {
+            const int j = idx / M2, c = idx - j * M2;
+            M[idx] = xo[(size_t)j * D + 2 + c];
+        }
     }
     if (tid < D) pcd[tid] = pconst_entry(a.consts, D, tid, tid, tg, Tt);
     __syncthreads();
     if (tid < M2) {   // sum of squares over all nodes: ssq[c<R] = sum U_c^2, ssq[R+c] = sum V_c^2
         double acc = 0.0;
         for (int j = 0; j < n; ++j) {
-            const double v = (double)M[j * M2 + tid];
+            const double v = (double)mrow(j, 0)[tid];
             acc = fma(v, v, acc);
         }
         ssq[tid] = acc;
@@ -208,14 +228,14 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             const int kc = ku ? R + ck : ck - R;
             double acc = 0.0;
             if (m < 2) {
-                for (int j = 1; j < n; ++j) acc += (double)M[j * M2 + kc];
+                for (int j = 1; j < n; ++j) acc += (double)mrow(j, 0)[kc];
                 v = (ku ? (m == 0 ? p : q) : (m == 0 ? q : s)) * acc;
             } else {
                 const int cm = m - 2;
                 const bool mu_ = cm < R;
                 const int mc = mu_ ? R + cm : cm - R;
                 for (int j = 1; j < n; ++j)
-                    acc = fma((double)M[j * M2 + kc], (double)M[j * M2 + mc], acc);
+                    acc = fma((double)mrow(j, 0)[kc], (double)mrow(j, 0)[mc], acc);
                 v = ((ku && mu_) ? p : ((!ku && !mu_) ? s : q)) * acc;
             }
         }
@@ -246,13 +266,13 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         K[k * KS + m] = -K[k * KS + m];
     }
 
-    double qiphi[MC], phitqi[MC];   // AR rows: thread (k = tid>>2, part = tid&3)
+    double qiphi[MC], phitqi[MC];   // AR rows: thread (k = tid / NPA, part = tid % NPA)
     {
-        const int k = tid >> 2, pp = tid & 3;
+        const int k = tid / NPA, pp = tid % NPA;
 #pragma unroll
         for (int mm = 0; mm < MC; ++mm) {
             const int m = pp * MC + mm;
-            const bool ok = (tid < 4 * D) && (m < D);
+            const bool ok = (tid < NPA * D) && (m < D);
             qiphi[mm] = ok ? a.consts[3 * DD + (size_t)k * D + m] : 0.0;
             phitqi[mm] = ok ? a.consts[4 * DD + (size_t)k * D + m] : 0.0;
         }
@@ -300,7 +320,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         const float2* yrow = (const float2*)(ysl + (size_t)node * n * 2);
         for (int j = tid + AME_NT * AME_YPF; j < n; j += AME_NT) put(j, yrow[j]);
     };
-    auto gemv = [&](int tw) {   // partial h_obs over node group (waves 1-3: tw < 192)
+    auto gemv = [&](int tw, int split) {   // partial h_obs over node group (waves 1-3: tw < 192)
         const int g = tw / CW, cq = tw - g * CW;
         if (g < GW) {
             const int c0 = cq * VEC;
@@ -314,8 +334,14 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             for (int j = g; j < n; j += GW) {
                 const float2 zz = z[j];
                 const float zc = upart ? zz.x : zz.y;
-                const float* mr = M + j * M2 + mo;
-                if constexpr (VEC == 4) {
+                const float* mr = mrow(j, split) + mo;
+                if constexpr (MG && VEC == 4) {   // rows are 8-byte aligned in HBM
+                    const float2 m0 = *(const float2*)mr, m1 = *(const float2*)(mr + 2);
+                    acc[0] = fmaf(zc, m0.x, acc[0]);
+                    acc[1] = fmaf(zc, m0.y, acc[1]);
+                    acc[2] = fmaf(zc, m1.x, acc[2]);
+                    acc[3] = fmaf(zc, m1.y, acc[3]);
+                } else if constexpr (VEC == 4) {
                     const float4 mv = *(const float4*)mr;
                     acc[0] = fmaf(zc, mv.x, acc[0]);
                     acc[1] = fmaf(zc, mv.y, acc[1]);
@@ -346,9 +372,9 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             gobs[(tid < M2) ? 2 + tid : tid - M2] = (double)acc;
         }
     };
-    auto ar_terms = [&]() {   // threads < 4D: ar = QiPhi mu_left + PhiTQi mu_right
-        if (tid < 4 * D) {
-            const int k = tid >> 2, pp = tid & 3;
+    auto ar_terms = [&]() {   // threads < NPA*D: ar = QiPhi mu_left + PhiTQi mu_right
+        if (tid < NPA * D) {
+            const int k = tid / NPA, pp = tid % NPA;
             double acc = 0.0;
 #pragma unroll
             for (int mm = 0; mm < MC; ++mm) {
@@ -359,30 +385,40 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 }
             }
             acc += __shfl_xor(acc, 1);
-            acc += __shfl_xor(acc, 2);
+            if constexpr (NPA == 4) acc += __shfl_xor(acc, 2);
             if (pp == 0) ar[k] = acc;
         }
     };
-    // wave 1: issue the granule loads of mu_{node,t-1}^new (returns when done or timed out)
-    auto poll_left = [&](int node, uint64_t first) {
-        const int k = lane;
+    // wave 1: wait for the granules of mu_{node,t-1}^new (returns when done or timed out);
+    // lane L owns state rows L + 64h
+    auto poll_left = [&](int node, const uint64_t (&first)[KH]) {
         const bool from_halo = (tl == 0);
         const uint64_t* src = from_halo ? a.halo_in + (size_t)node * D
                                         : a.hand + ((size_t)(tl - 1) * n + node) * D;
-        uint64_t v = first;
-        bool ok = (k >= D) || (uint32_t)(v >> 32) == a.epoch;
+        uint64_t v[KH];
+        bool ok = true;
+#pragma unroll
+        for (int h = 0; h < KH; ++h) {
+            v[h] = first[h];
+            if (lane + 64 * h < D) ok = ok && (uint32_t)(v[h] >> 32) == a.epoch;
+        }
         if (!__all(ok) && !dead) {
             const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
             const uint64_t budget = from_halo ? AME_SPIN_TICKS_HALO : AME_SPIN_TICKS_LOCAL;
             while (true) {
                 __builtin_amdgcn_s_sleep(2);
-                if (k < D) {
-                    v = from_halo ? gran_load_system(src + k) : gran_load_agent(src + k);
-                    ok = (uint32_t)(v >> 32) == a.epoch;
+                ok = true;
+#pragma unroll
+                for (int h = 0; h < KH; ++h) {
+                    const int k = lane + 64 * h;
+                    if (k < D) {
+                        v[h] = from_halo ? gran_load_system(src + k) : gran_load_agent(src + k);
+                        ok = ok && (uint32_t)(v[h] >> 32) == a.epoch;
+                    }
                 }
                 if (__all(ok)) break;
                 if (__builtin_amdgcn_s_memrealtime() - t_start > budget) {
-                    if (k == 0)
+                    if (lane == 0)
                         atomicOr(a.status, from_halo ? AME_STATUS_HALO_TIMEOUT
                                                      : AME_STATUS_SPIN_TIMEOUT);
                     dead = true;
@@ -390,14 +426,25 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 }
             }
         }
-        if (k < D) mu_left[k] = __uint_as_float((uint32_t)v);
+#pragma unroll
+        for (int h = 0; h < KH; ++h)
+            if (lane + 64 * h < D) mu_left[lane + 64 * h] = __uint_as_float((uint32_t)v[h]);
     };
-    auto first_poll = [&](int node) -> uint64_t {   // wave 1: issue the first granule loads
-        if (tg == 0 || lane >= D) return 0;
+    auto first_poll = [&](int node, uint64_t (&g)[KH]) {   // wave 1: issue the first granule loads
         const bool from_halo = (tl == 0);
         const uint64_t* src = from_halo ? a.halo_in + (size_t)node * D
                                         : a.hand + ((size_t)(tl - 1) * n + node) * D;
-        return from_halo ? gran_load_system(src + lane) : gran_load_agent(src + lane);
+#pragma unroll
+        for (int h = 0; h < KH; ++h) {
+            const int k = lane + 64 * h;
+            g[h] = 0;
+            if (tg > 0 && k < D) g[h] = from_halo ? gran_load_system(src + k) : gran_load_agent(src + k);
+        }
+    };
+    auto zero_left = [&]() {   // wave 1, global slice 0: no left neighbour
+#pragma unroll
+        for (int h = 0; h < KH; ++h)
+            if (lane + 64 * h < D) mu_left[lane + 64 * h] = 0.f;
     };
     auto right_regs = [&](int node, float& nx, float& ol) {   // threads 128..128+D
         const int k = tid - 128;
@@ -415,8 +462,13 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         if (tid >= 128 && tid < 128 + D) right_regs(0, nx, ol);
         stage_z(0, -1);
         if (wave == 1) {
-            if (tg > 0) poll_left(0, first_poll(0));
-            else if (lane < D) mu_left[lane] = 0.f;
+            if (tg > 0) {
+                uint64_t g0[KH];
+                first_poll(0, g0);
+                poll_left(0, g0);
+            } else {
+                zero_left();
+            }
         }
         if (tid >= 128 && tid < 128 + D) {
             mu_right[tid - 128] = nx;
@@ -425,7 +477,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     }
     if (n > 1) prefetch_y(1);
     __syncthreads();
-    if (wave >= 1) gemv(tid - 64);
+    if (wave >= 1) gemv(tid - 64, 0);
     __syncthreads();
     gemv_reduce();
     ar_terms();
@@ -453,9 +505,9 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         }
         // ---------------- phase 1 ----------------
         if (has_prev && tid < M2) {   // node i-1: statistics and slice (U,V) <- new
-            const double vo = (double)M[(i - 1) * M2 + tid], vn = (double)mu_prev[2 + tid];
+            const double vo = (double)mrow(i - 1, i - 1)[tid], vn = (double)mu_prev[2 + tid];
             ssq[tid] = ssq[tid] - vo * vo + vn * vn;
-            M[(i - 1) * M2 + tid] = mu_prev[2 + tid];
+            if constexpr (!MG) M[(i - 1) * M2 + tid] = mu_prev[2 + tid];
         }
         {
             constexpr int NIT = 4 * D + (1 + US) * D;
@@ -469,7 +521,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                     const bool prevv = qv < 2;
                     if (prevv ? has_prev : has_next) {
                         const bool row0 = (qv & 1) == 0;   // e0 = [1,0,V,0] ; e1 = [0,1,0,U]
-                        const float* src = prevv ? (mu_prev + 2) : (M + (i + 1) * M2);
+                        const float* src = prevv ? (mu_prev + 2) : mrow(i + 1, i + 1);
                         const int cb = row0 ? 2 : 2 + R;
                         const float* vv = row0 ? (src + R) : src;
                         acc = K[k * KS + (row0 ? 0 : 1)];
@@ -495,120 +547,168 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             if (has_next) stage_z(i + 1, i);
             STAMPW(7, 0);
         }
+        // MG: node i-1's new mean (xn, stored by wave 0 in the previous step) is
+        // read by this step's GEMV in waves 1-3: drain it before the barrier
+        if constexpr (MG) {
+            if (wave == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         lds_barrier();   // B1
         STAMP(1);
         // ---------------- phase 2 ----------------
         if (wave == 0) {
-            const int k = lane;
-            const bool kl = k < D;
-            double W0 = 0, W1 = 0, Y0 = 0, Y1 = 0, ua = 0, uM = 0, gk = 0, K0 = 0, K1 = 0;
-            double jp0 = 0, jp1 = 0, jn0 = 0, jn1 = 0;
-            if (kl) {
-                W0 = vec[k]; W1 = vec[D + k]; Y0 = vec[2 * D + k]; Y1 = vec[3 * D + k];
-                ua = vec[4 * D + k];
+            // lane owns state rows k = lane + 64h (h < KH)
+            double W0[KH], W1[KH], Y0[KH], Y1[KH], ua[KH], uM[KH], gk[KH], K0[KH], K1[KH];
+            double jp0[KH], jp1[KH], jn0[KH], jn1[KH];
+            const float* mnext = has_next ? mrow(i + 1, i + 1) : nullptr;
 #pragma unroll
-                for (int ch = 0; ch < US; ++ch) uM += vec[(5 + ch) * D + k];
-                gk = gobs[k] + ar[k];
-                K0 = K[k * KS + 0];
-                K1 = K[k * KS + 1];
-                if (k == 0) { jp0 = 1.0; jn0 = 1.0; }
-                if (k == 1) { jp1 = 1.0; jn1 = 1.0; }
-                if (k >= 2 && k < 2 + R) {
-                    jp0 = (double)mu_prev[2 + R + (k - 2)];
-                    if (has_next) jn0 = (double)M[(i + 1) * M2 + R + (k - 2)];
-                }
-                if (k >= 2 + R) {
-                    jp1 = (double)mu_prev[2 + (k - 2 - R)];
-                    if (has_next) jn1 = (double)M[(i + 1) * M2 + (k - 2 - R)];
+            for (int h = 0; h < KH; ++h) {
+                const int k = lane + 64 * h;
+                W0[h] = W1[h] = Y0[h] = Y1[h] = ua[h] = uM[h] = gk[h] = K0[h] = K1[h] = 0;
+                jp0[h] = jp1[h] = jn0[h] = jn1[h] = 0;
+                if (k < D) {
+                    W0[h] = vec[k]; W1[h] = vec[D + k]; Y0[h] = vec[2 * D + k]; Y1[h] = vec[3 * D + k];
+                    ua[h] = vec[4 * D + k];
+#pragma unroll
+                    for (int ch = 0; ch < US; ++ch) uM[h] += vec[(5 + ch) * D + k];
+                    gk[h] = gobs[k] + ar[k];
+                    K0[h] = K[k * KS + 0];
+                    K1[h] = K[k * KS + 1];
+                    if (k == 0) { jp0[h] = 1.0; jn0[h] = 1.0; }
+                    if (k == 1) { jp1[h] = 1.0; jn1[h] = 1.0; }
+                    if (k >= 2 && k < 2 + R) {
+                        jp0[h] = (double)mu_prev[2 + R + (k - 2)];
+                        if (has_next) jn0[h] = (double)mnext[R + (k - 2)];
+                    }
+                    if (k >= 2 + R) {
+                        jp1[h] = (double)mu_prev[2 + (k - 2 - R)];
+                        if (has_next) jn1[h] = (double)mnext[k - 2 - R];
+                    }
                 }
             }
-            const double u = ua + uM;
             const double z0 = r00 * (double)y_prev0 + r01 * (double)y_prev1;
             const double z1 = r10 * (double)y_prev0 + r11 * (double)y_prev1;
-            const double hk = has_prev ? gk + jp0 * z0 + jp1 * z1 : gk;   // natural parameter
-            double mus;
-            double Lp0 = 0, Lp1 = 0, Rp0 = 0, Rp1 = 0;   // P_i^-1 = K - Lp Rp^T
-            double Xp0 = Y0, Xp1 = Y1;                   // X' = P_i^-1 J_{i+1}^T
+            double u[KH], hk[KH], mus[KH];
+            double Lp0[KH], Lp1[KH], Rp0[KH], Rp1[KH];   // P_i^-1 = K - Lp Rp^T
+            double Xp0[KH], Xp1[KH];                     // X' = P_i^-1 J_{i+1}^T
+#pragma unroll
+            for (int h = 0; h < KH; ++h) {
+                u[h] = ua[h] + uM[h];
+                hk[h] = has_prev ? gk[h] + jp0[h] * z0 + jp1[h] * z1 : gk[h];   // natural parameter
+                Lp0[h] = Lp1[h] = Rp0[h] = Rp1[h] = 0;
+                Xp0[h] = Y0[h];
+                Xp1[h] = Y1[h];
+            }
             if (has_prev) {
-                double pr[14], o[14];
-                pr[0] = jp0 * W0; pr[1] = jp0 * W1; pr[2] = jp1 * W0; pr[3] = jp1 * W1;
-                pr[4] = jp0 * u;  pr[5] = jp1 * u;
-                pr[6] = jp0 * Y0; pr[7] = jp0 * Y1; pr[8] = jp1 * Y0; pr[9] = jp1 * Y1;
-                pr[10] = jp0 * ua; pr[11] = jp1 * ua; pr[12] = jp0 * uM; pr[13] = jp1 * uM;
-                wave_multidot<14, D>(pr, o, red, scal, lane);
+                double pr[KH][14], o[14];
+#pragma unroll
+                for (int h = 0; h < KH; ++h) {
+                    pr[h][0] = jp0[h] * W0[h]; pr[h][1] = jp0[h] * W1[h];
+                    pr[h][2] = jp1[h] * W0[h]; pr[h][3] = jp1[h] * W1[h];
+                    pr[h][4] = jp0[h] * u[h];  pr[h][5] = jp1[h] * u[h];
+                    pr[h][6] = jp0[h] * Y0[h]; pr[h][7] = jp0[h] * Y1[h];
+                    pr[h][8] = jp1[h] * Y0[h]; pr[h][9] = jp1[h] * Y1[h];
+                    pr[h][10] = jp0[h] * ua[h]; pr[h][11] = jp1[h] * ua[h];
+                    pr[h][12] = jp0[h] * uM[h]; pr[h][13] = jp1[h] * uM[h];
+                }
+                wave_multidot<14, D, KH>(pr, o, red, scal, lane);
                 STAMPW(8, 0);
                 M22 Mm = {Rm.a + o[0], Rm.b + 0.5 * (o[1] + o[2]), 0.0, Rm.d + o[3]};
                 Mm.c = Mm.b;
                 M22 Mi = inv22(Mm);
                 Mi.b = Mi.c = 0.5 * (Mi.b + Mi.c);
-                const double wm0 = W0 * Mi.a + W1 * Mi.c, wm1 = W0 * Mi.b + W1 * Mi.d;
-                Lp0 = wm0; Lp1 = wm1; Rp0 = W0; Rp1 = W1;
-                if (!is_bad) {
-                    mus = u + wm0 * ((double)y_prev0 - o[4]) + wm1 * ((double)y_prev1 - o[5]);
-                } else {
-                    // P^-1 h^(x) = K h^(x) - W M^-1 (J K h^(x)); J K[:,b] = (W0[b], W1[b])
-                    const double Wa00 = __shfl(W0, 0), Wa01 = __shfl(W0, 1);
-                    const double Wa10 = __shfl(W1, 0), Wa11 = __shfl(W1, 1);
-                    const double ta = ua + z0 * K0 + z1 * K1;
-                    const double tM = uM + z0 * (W0 - K0) + z1 * (W1 - K1);
-                    if (k < 2) {
-                        const double j0 = o[10] + z0 * Wa00 + z1 * Wa01;
-                        const double j1 = o[11] + z0 * Wa10 + z1 * Wa11;
-                        mus = ta - (wm0 * j0 + wm1 * j1);
+                // rows 0, 1 of W (J K[:,b] = (W0[b], W1[b])) live in lanes 0, 1 of h = 0
+                const double Wa00 = __shfl(W0[0], 0), Wa01 = __shfl(W0[0], 1);
+                const double Wa10 = __shfl(W1[0], 0), Wa11 = __shfl(W1[0], 1);
+#pragma unroll
+                for (int h = 0; h < KH; ++h) {
+                    const int k = lane + 64 * h;
+                    const double wm0 = W0[h] * Mi.a + W1[h] * Mi.c, wm1 = W0[h] * Mi.b + W1[h] * Mi.d;
+                    Lp0[h] = wm0; Lp1[h] = wm1; Rp0[h] = W0[h]; Rp1[h] = W1[h];
+                    if (!is_bad) {
+                        mus[h] = u[h] + wm0 * ((double)y_prev0 - o[4]) + wm1 * ((double)y_prev1 - o[5]);
                     } else {
-                        const double j0 = o[12] + z0 * (o[0] - Wa00) + z1 * (o[1] - Wa01);
-                        const double j1 = o[13] + z0 * (o[2] - Wa10) + z1 * (o[3] - Wa11);
-                        mus = tM - (wm0 * j0 + wm1 * j1);
+                        // P^-1 h^(x) = K h^(x) - W M^-1 (J K h^(x))
+                        const double ta = ua[h] + z0 * K0[h] + z1 * K1[h];
+                        const double tM = uM[h] + z0 * (W0[h] - K0[h]) + z1 * (W1[h] - K1[h]);
+                        if (k < 2) {
+                            const double j0 = o[10] + z0 * Wa00 + z1 * Wa01;
+                            const double j1 = o[11] + z0 * Wa10 + z1 * Wa11;
+                            mus[h] = ta - (wm0 * j0 + wm1 * j1);
+                        } else {
+                            const double j0 = o[12] + z0 * (o[0] - Wa00) + z1 * (o[1] - Wa01);
+                            const double j1 = o[13] + z0 * (o[2] - Wa10) + z1 * (o[3] - Wa11);
+                            mus[h] = tM - (wm0 * j0 + wm1 * j1);
+                        }
                     }
+                    Xp0[h] = Y0[h] - (wm0 * o[6] + wm1 * o[8]);
+                    Xp1[h] = Y1[h] - (wm0 * o[7] + wm1 * o[9]);
                 }
-                Xp0 = Y0 - (wm0 * o[6] + wm1 * o[8]);
-                Xp1 = Y1 - (wm0 * o[7] + wm1 * o[9]);
             } else {
-                mus = is_bad ? ((k < 2) ? ua : uM) : u;
+#pragma unroll
+                for (int h = 0; h < KH; ++h)
+                    mus[h] = is_bad ? ((lane + 64 * h < 2) ? ua[h] : uM[h]) : u[h];
             }
-            if (!is_naive) mus += 1e-6 * hk;
-            if (kl) {   // damped new mean; publish (mu_prev: readers above are done, wave-ordered)
-                const float nw = __fadd_rn(__fmul_rn(lr, (float)mus), __fmul_rn(om, mu_old[k]));
-                xn[(size_t)i * D + k] = nw;
-                mu_prev[k] = nw;
-                const uint64_t g = ((uint64_t)a.epoch << 32) | (uint64_t)__float_as_uint(nw);
-                gran_store_agent(a.hand + ((size_t)tl * n + i) * D + k, g);
-                if (tl == TL - 1 && a.halo_out != nullptr)
-                    gran_store_system(a.halo_out + (size_t)i * D + k, g);
+#pragma unroll
+            for (int h = 0; h < KH; ++h) {
+                const int k = lane + 64 * h;
+                if (!is_naive) mus[h] += 1e-6 * hk[h];
+                if (k < D) {   // damped new mean; publish (mu_prev: readers above are done, wave-ordered)
+                    const float nw = __fadd_rn(__fmul_rn(lr, (float)mus[h]), __fmul_rn(om, mu_old[k]));
+                    xn[(size_t)i * D + k] = nw;
+                    mu_prev[k] = nw;
+                    const uint64_t g = ((uint64_t)a.epoch << 32) | (uint64_t)__float_as_uint(nw);
+                    gran_store_agent(a.hand + ((size_t)tl * n + i) * D + k, g);
+                    if (tl == TL - 1 && a.halo_out != nullptr)
+                        gran_store_system(a.halo_out + (size_t)i * D + k, g);
+                }
             }
             STAMPW(9, 0);
-            double Lm0 = 0, Lm1 = 0, Rm0 = 0, Rm1 = 0;   // downdate: + X' S'^-1 X'^T
+            double Lm0[KH], Lm1[KH], Rm0[KH], Rm1[KH];   // downdate: + X' S'^-1 X'^T
+#pragma unroll
+            for (int h = 0; h < KH; ++h) Lm0[h] = Lm1[h] = Rm0[h] = Rm1[h] = 0;
             if (has_next) {
-                double pr2[4], o2[4];
-                pr2[0] = jn0 * Xp0; pr2[1] = jn0 * Xp1; pr2[2] = jn1 * Xp0; pr2[3] = jn1 * Xp1;
-                wave_multidot<4, D>(pr2, o2, red, scal + 16, lane);
+                double pr2[KH][4], o2[4];
+#pragma unroll
+                for (int h = 0; h < KH; ++h) {
+                    pr2[h][0] = jn0[h] * Xp0[h]; pr2[h][1] = jn0[h] * Xp1[h];
+                    pr2[h][2] = jn1[h] * Xp0[h]; pr2[h][3] = jn1[h] * Xp1[h];
+                }
+                wave_multidot<4, D, KH>(pr2, o2, red, scal + 16, lane);
                 M22 Sm = {Rm.a - o2[0], Rm.b - 0.5 * (o2[1] + o2[2]), 0.0, Rm.d - o2[3]};
                 Sm.c = Sm.b;
                 M22 Si = inv22(Sm);
                 Si.b = Si.c = 0.5 * (Si.b + Si.c);
-                Lm0 = Xp0 * Si.a + Xp1 * Si.c;
-                Lm1 = Xp0 * Si.b + Xp1 * Si.d;
-                Rm0 = Xp0;
-                Rm1 = Xp1;
+#pragma unroll
+                for (int h = 0; h < KH; ++h) {
+                    Lm0[h] = Xp0[h] * Si.a + Xp1[h] * Si.c;
+                    Lm1[h] = Xp0[h] * Si.b + Xp1[h] * Si.d;
+                    Rm0[h] = Xp0[h];
+                    Rm1[h] = Xp1[h];
+                }
             }
             STAMPW(10, 0);
-            if (kl) {
-                upd[k] = Lp0; upd[D + k] = Lp1; upd[2 * D + k] = Rp0; upd[3 * D + k] = Rp1;
-                upd[4 * D + k] = Lm0; upd[5 * D + k] = Lm1; upd[6 * D + k] = Rm0; upd[7 * D + k] = Rm1;
+#pragma unroll
+            for (int h = 0; h < KH; ++h) {
+                const int k = lane + 64 * h;
+                if (k < D) {
+                    upd[k] = Lp0[h]; upd[D + k] = Lp1[h]; upd[2 * D + k] = Rp0[h]; upd[3 * D + k] = Rp1[h];
+                    upd[4 * D + k] = Lm0[h]; upd[5 * D + k] = Lm1[h];
+                    upd[6 * D + k] = Rm0[h]; upd[7 * D + k] = Rm1[h];
+                }
             }
         } else if (has_next) {
             // waves 1-3: next-node loads first (latency hidden by the GEMV), GEMV, then hand-offs
             float nx = 0.f, ol = 0.f;
             if (tid >= 128 && tid < 128 + D) right_regs(i + 1, nx, ol);
-            uint64_t g0 = 0;
-            if (wave == 1 && tg > 0) g0 = first_poll(i + 1);
+            uint64_t g0[KH];
+            if (wave == 1) first_poll(i + 1, g0);
             if (i + 2 < n) prefetch_y(i + 2);
-            gemv(tid - 64);
+            gemv(tid - 64, i);
             STAMPW(11, 64);
             STAMPW(13, 128);
             if (wave == 1) {
                 if (tg > 0) poll_left(i + 1, g0);
-                else if (lane < D) mu_left[lane] = 0.f;
+                else zero_left();
                 STAMPW(12, 64);
             }
             if (tid >= 128 && tid < 128 + D) {
@@ -638,10 +738,10 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                         if (k == 0) pd = p * (double)(n - 1);
                         else if (k == 1) pd = s * (double)(n - 1);
                         else if (k < 2 + R) {
-                            const double vo = (double)M[i * M2 + R + (k - 2)];
+                            const double vo = (double)mrow(i, i)[R + (k - 2)];
                             pd = p * (ssq[R + (k - 2)] - vo * vo);
                         } else {
-                            const double uo = (double)M[i * M2 + (k - 2 - R)];
+                            const double uo = (double)mrow(i, i)[k - 2 - R];
                             pd = s * (ssq[k - 2 - R] - uo * uo);
                         }
                         c32 = 1.0f / ((float)(pd + pcd[k]) + 1e-8f);
@@ -673,10 +773,10 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     }
 }
 
-template <int R>
-static int launch_sweep(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {
-    const SweepLds L = sweep_lds_layout(dm->n, R);
-    auto kern = ame_sweep_kernel<R>;
+template <int R, bool MG>
+static int launch_sweep_t(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {
+    const SweepLds L = sweep_lds_layout(dm->n, R, MG ? 1 : 0);
+    auto kern = ame_sweep_kernel<R, MG>;
     if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)L.total) != hipSuccess)
         return -2;
@@ -685,9 +785,16 @@ static int launch_sweep(const ame_dims* dm, const ame_sweep_args* a, hipStream_t
 }
 
 template <int R>
-static int sweep_occupancy(int n) {
-    const SweepLds L = sweep_lds_layout(n, R);
-    auto kern = ame_sweep_kernel<R>;
+static int launch_sweep(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {
+    if (sweep_lds_layout(dm->n, R, ame_sweep_force_global()).m_global)
+        return launch_sweep_t<R, true>(dm, a, st);
+    return launch_sweep_t<R, false>(dm, a, st);
+}
+
+template <int R, bool MG>
+static int sweep_occupancy_t(int n) {
+    const SweepLds L = sweep_lds_layout(n, R, MG ? 1 : 0);
+    auto kern = ame_sweep_kernel<R, MG>;
     if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)L.total) != hipSuccess)
         return 0;
@@ -696,6 +803,12 @@ static int sweep_occupancy(int n) {
         hipSuccess)
         return 0;
     return per_cu;
+}
+
+template <int R>
+static int sweep_occupancy(int n) {
+    if (sweep_lds_layout(n, R, ame_sweep_force_global()).m_global) return sweep_occupancy_t<R, true>(n);
+    return sweep_occupancy_t<R, false>(n);
 }
 
 int ame_sweep_dispatch(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {

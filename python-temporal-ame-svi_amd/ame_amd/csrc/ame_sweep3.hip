@@ -1108,6 +1108,9 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
 }
 
 
+// v3 keeps one state row per solver lane: D = 2 + 2r <= 64.
+constexpr int kV3MaxR = 31;
+
 template <int R>
 static int l3_total(int n) { return Lay<R>::total(n, Cfg<R>::NSREG); }
 
@@ -1127,7 +1130,7 @@ static int sweep3_occupancy(int n) {
 int ame_sweep3_blocks_per_cu(int n, int r) {
     switch (r) {
 #define X(RR) \
-    case RR: return sweep3_occupancy<RR>(n);
+    case RR: if constexpr (RR <= kV3MaxR) return sweep3_occupancy<RR>(n); else return 0;
         AME_FOR_EACH_R(X)
 #undef X
         default: return 0;
@@ -1148,7 +1151,7 @@ static int sweep3_fits(int n) {
 int ame_sweep3_supported(int n, int r) {
     switch (r) {
 #define X(RR) \
-    case RR: return sweep3_fits<RR>(n);
+    case RR: if constexpr (RR <= kV3MaxR) return sweep3_fits<RR>(n); else return 0;
         AME_FOR_EACH_R(X)
 #undef X
         default: return 0;
@@ -1169,7 +1172,7 @@ static int launch_sweep3(const ame_dims* dm, const ame_sweep_args* a, hipStream_
 int ame_sweep3_dispatch(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {
     switch (dm->r) {
 #define X(RR) \
-    case RR: return launch_sweep3<RR>(dm, a, st);
+    case RR: if constexpr (RR <= kV3MaxR) return launch_sweep3<RR>(dm, a, st); else return -1;
         AME_FOR_EACH_R(X)
 #undef X
         default: return -1;

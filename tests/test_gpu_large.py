@@ -1,0 +1,123 @@
+"""GPU parity of the v2 sweep's wide and large modes, through the C-ABI:
+
+* r = 32 (d = 66 > 64: two state rows per solver lane), BASELINE config 5's
+  latent dim, against the fp64 oracle on small problems, all three variants;
+* the slice's (U,V) block read from HBM instead of LDS (forced with
+  AME_SWEEP_M_GLOBAL=1 at small n; automatic at n = 4096);
+* config 5's node count and latent dim (n = 4096, r = 32) on a few slices:
+  the first nodes of the Gauss-Seidel sweep against the oracle replaying the
+  same sweep prefix (node i depends only on the initial state and on nodes < i,
+  Appendix B of SURVEY.md), and the ELBO / MSE of the device state against the
+  oracle's ELBO of that same state.
+
+Tolerances as in test_gpu_parity.py: 5e-6 relative vs the fp64 oracle, or no
+further from it than the reference's own fp32 arithmetic (fp32 oracle) is.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+PKEYS = ("R", "R_inv", "Sigma", "Psi", "Phi", "Q")
+
+
+def _vi(model, method, lr, dev):
+    from ame_amd import TemporalAMENaiveMFVI, TemporalAMEStructuredMFVI
+    if method == "naive":
+        return TemporalAMENaiveMFVI(model, learning_rate=lr, device=dev)
+    return TemporalAMEStructuredMFVI(model, factorization=method, learning_rate=lr, device=dev)
+
+
+def _params(m, dtype=np.float64):
+    return {k: getattr(m, k).numpy().astype(dtype) for k in PKEYS}
+
+
+def _check_vs_oracle(n, T, r, method, lr, dev, iters=2):
+    import ame_oracle as O
+    from ame_amd import TemporalAMEModel
+    m = TemporalAMEModel(n, T, r, seed=7)
+    m.generate_data_fast(seed=11)
+    vi = _vi(m, method, lr, dev)
+    Xm = vi.X_mean.numpy().astype(np.float64).copy()
+    Xc = vi.X_cov.numpy().astype(np.float64).copy()
+    Xm32, Xc32 = vi.X_mean.numpy().copy(), vi.X_cov.numpy().copy()
+    params = _params(m)
+    ref = O.fit(m.Y.numpy().astype(np.float64), Xm, Xc, params, method, lr, iters, 0.0)
+    O.fit(m.Y.numpy(), Xm32, Xc32, _params(m, np.float32), method, lr, iters, 0.0)
+    fp32_err = np.abs(Xm32.astype(np.float64) - Xm).max()
+    h = vi.fit(max_iter=iters, tolerance=0.0, verbose=False)
+    err = np.abs(vi.X_mean.numpy() - Xm).max()
+    assert err <= max(5e-6 * max(1.0, np.abs(Xm).max()), fp32_err), (err, fp32_err)
+    cerr = np.abs(vi.X_cov.numpy() - Xc).max()
+    assert cerr <= 1e-6 * max(1.0, np.abs(Xc).max()), cerr
+    for a, b in zip(h["elbo"], ref["elbo"]):
+        assert abs(float(a) - b) <= 5e-6 * abs(b), (float(a), b)
+    for a, b in zip(h["reconstruction_error"], ref["reconstruction_error"]):
+        assert abs(a - b) <= 5e-6 * abs(b), (a, b)
+    return vi
+
+
+@pytest.mark.parametrize("n,T,r,method,lr", [
+    (24, 3, 32, "good", 0.5), (20, 4, 32, "bad", 1.0), (22, 3, 32, "naive", 0.3),
+    (2, 2, 32, "good", 1.0), (40, 1, 32, "good", 0.01)])
+def test_r32_vs_oracle(n, T, r, method, lr, gpu_device):
+    """d = 66: the solver wave holds rows 64, 65 in a second register set."""
+    vi = _check_vs_oracle(n, T, r, method, lr, gpu_device)
+    assert vi.engine.r == 32
+
+
+@pytest.mark.parametrize("n,T,r,method,lr", [
+    (50, 4, 4, "good", 0.5), (37, 3, 5, "bad", 1.0), (45, 3, 16, "naive", 0.7),
+    (30, 3, 32, "good", 0.5), (700, 2, 16, "good", 0.5)])
+def test_global_slice_vs_oracle(n, T, r, method, lr, gpu_device, monkeypatch):
+    """(U,V) block in HBM (AME_SWEEP_M_GLOBAL=1) on the v2 sweep (AME_SWEEP_V2=1)."""
+    monkeypatch.setenv("AME_SWEEP_V2", "1")
+    monkeypatch.setenv("AME_SWEEP_M_GLOBAL", "1")
+    _check_vs_oracle(n, T, r, method, lr, gpu_device)
+
+
+@pytest.mark.parametrize("n,T,r,method,lr", [(64, 5, 8, "good", 0.5), (33, 4, 3, "bad", 1.0)])
+def test_v2_lds_slice_vs_oracle(n, T, r, method, lr, gpu_device, monkeypatch):
+    """The v2 sweep with the slice in LDS (the path r = 32 takes at small n)."""
+    monkeypatch.setenv("AME_SWEEP_V2", "1")
+    _check_vs_oracle(n, T, r, method, lr, gpu_device)
+
+
+@pytest.mark.parametrize("method", ["good", "bad", "naive"])
+def test_config5_shape_prefix_and_elbo(method, gpu_device):
+    """n = 4096, r = 32 (config 5), 3 slices: the first 3 nodes of one sweep
+    against the oracle's replay of the same prefix, and the device ELBO / MSE
+    against the oracle's ELBO of the device state."""
+    import ame_oracle as O
+    from ame_amd import TemporalAMEModel
+    n, T, r, lr, k = 4096, 3, 32, 0.5, 3
+    m = TemporalAMEModel(n, T, r, seed=5)
+    m.generate_data_fast(seed=6)
+    vi = _vi(m, method, lr, gpu_device)
+    assert not vi.engine.pipelined   # v2 sweep with the slice in HBM
+    Y64 = m.Y.numpy().astype(np.float64)
+    Y32 = m.Y.numpy()
+    Xm = vi.X_mean.numpy().astype(np.float64).copy()
+    Xc = vi.X_cov.numpy().astype(np.float64).copy()
+    Xm32, Xc32 = vi.X_mean.numpy().copy(), vi.X_cov.numpy().copy()
+    p64, p32 = _params(m), _params(m, np.float32)
+    c64, c32 = O.prior_terms(p64, T, np.float64), O.prior_terms(p32, T, np.float32)
+    for i in range(k):
+        O.update_node(Y64, Xm, Xc, p64, i, method, lr, c64)
+        O.update_node(Y32, Xm32, Xc32, p32, i, method, lr, c32)
+    h = vi.fit(max_iter=1, tolerance=0.0, verbose=False)
+    got_m = vi.X_mean.numpy()[:k].astype(np.float64)
+    got_c = vi.X_cov.numpy()[:k].astype(np.float64)
+    fp32_err = np.abs(Xm32[:k].astype(np.float64) - Xm[:k]).max()
+    err = np.abs(got_m - Xm[:k]).max()
+    assert err <= max(5e-6 * max(1.0, np.abs(Xm[:k]).max()), fp32_err), (err, fp32_err)
+    cerr = np.abs(got_c - Xc[:k]).max()
+    assert cerr <= 1e-6 * max(1.0, np.abs(Xc[:k]).max()), cerr
+    # ELBO / MSE kernels at full size on the device's own post-sweep state
+    Sm = vi.X_mean.numpy()
+    Sc = vi.X_cov.numpy()
+    e_ref = O.elbo(Y64, Sm, Sc, p64, method)
+    mse_ref = O.recon_error(Y64, Sm)
+    assert np.isfinite(float(h["elbo"][0]))
+    assert abs(float(h["elbo"][0]) - e_ref) <= 5e-6 * abs(e_ref), (float(h["elbo"][0]), e_ref)
+    assert abs(h["reconstruction_error"][0] - mse_ref) <= 5e-6 * mse_ref
