@@ -168,6 +168,27 @@ long long ame_elbo_work_size(const ame_dims* dims);
 int ame_host_register(void* host, unsigned long long bytes, void** dev);
 int ame_host_unregister(void* host);
 
+/* ---- post-fit alignment -------------------------------
+ * Replaces the per-time-step loops of src/utils/alignment.py:
+ * align_temporal_states (:224-321) and compute_alignment_error (:324-385).
+ * x_est, x_true: (n, T, d) fp32 device arrays, d = 2 + 2r.
+ * ame_align_cross: global_mode = 0 -> cross[T][2][r][r] = U_true^T U_est and
+ *   V_true^T V_est per time step (alignment.py:76, called from :211-212);
+ *   global_mode = 1 -> cross[2r][2r] = Mbar_true^T Mbar_est of the time-averaged
+ *   (U,V) blocks (:293-303), using work (ame_align_work_size doubles).
+ * The caller turns each cross block into R = U Vt (svd, det(R) < 0 -> last
+ * row of Vt negated, :79-87) and passes the rotations to
+ * ame_align_apply: x_out = sign-aligned x_est (additive pair by row sign,
+ *   (U,V) rotated then sign-aligned per row, :275-289 / :306-319) and
+ *   partials[ame_align_partials_size] = fp64 partial sums of |x_out - x_true|^2. */
+long long ame_align_work_size(int n, int T, int r);
+long long ame_align_cross_size(int n, int T, int r, int global_mode);
+long long ame_align_partials_size(int n, int T);
+int ame_align_cross(const float* x_est, const float* x_true, int n, int T, int r, int global_mode,
+                    double* cross, double* work, void* stream);
+int ame_align_apply(const float* x_est, const float* x_true, int n, int T, int r, int global_mode,
+                    const double* rot, float* x_out, double* partials, void* stream);
+
 /* Latent dims compiled into this library (fills up to cap entries, returns count). */
 int ame_supported_r(int* out, int cap);
 

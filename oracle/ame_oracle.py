@@ -315,3 +315,69 @@ def fit(Y, X_mean, X_cov, params, variant, lr, max_iter, tolerance=1e-4):
         if converged:
             break
     return hist
+
+
+# ----------------------------------------------------------------------------
+# post-fit alignment (src/utils/alignment.py), SURVEY §8f row f4
+# ----------------------------------------------------------------------------
+def procrustes_alignment(X_est, X_true):
+    """alignment.py:75-90: R = U Vt of svd(X_true^T X_est), last row of Vt
+    negated when det(R) < 0; returns (X_est R, R)."""
+    M = X_true.T @ X_est
+    U, _, Vt = np.linalg.svd(M)
+    R = U @ Vt
+    if np.linalg.det(R) < 0:
+        Vt = Vt.copy()
+        Vt[-1, :] *= -1
+        R = U @ Vt
+    return X_est @ R, R
+
+
+def align_signs_rows(X_est, X_true):
+    """alignment.py:137-145 (dim = last): flip row i when -x_i is closer."""
+    out = X_est.copy()
+    for i in range(X_est.shape[0]):
+        if np.linalg.norm(-X_est[i] - X_true[i]) < np.linalg.norm(X_est[i] - X_true[i]):
+            out[i] = -out[i]
+    return out
+
+
+def align_latent_positions(M_est, M_true, r):
+    """alignment.py:202-221: Procrustes on U and on V separately, then row signs."""
+    U, _ = procrustes_alignment(M_est[:, :r], M_true[:, :r])
+    V, _ = procrustes_alignment(M_est[:, r:], M_true[:, r:])
+    return np.concatenate([align_signs_rows(U, M_true[:, :r]),
+                           align_signs_rows(V, M_true[:, r:])], axis=1)
+
+
+def align_temporal_states(X_est, X_true, r, align_each_time=True):
+    """alignment.py:265-321."""
+    n, T, d = X_est.shape
+    out = X_est.copy()
+    if align_each_time:
+        for t in range(T):
+            out[:, t, :2] = align_signs_rows(X_est[:, t, :2], X_true[:, t, :2])
+            out[:, t, 2:] = align_latent_positions(X_est[:, t, 2:], X_true[:, t, 2:], r)
+    else:
+        _, RM = procrustes_alignment(X_est.mean(axis=1)[:, 2:], X_true.mean(axis=1)[:, 2:])
+        for t in range(T):
+            out[:, t, :2] = align_signs_rows(X_est[:, t, :2], X_true[:, t, :2])
+            out[:, t, 2:] = align_signs_rows(X_est[:, t, 2:] @ RM, X_true[:, t, 2:])
+    return out
+
+
+def compute_alignment_error(X_est, X_true, r, align=True):
+    """alignment.py:359-385, temporal (n, T, d) inputs."""
+    Xa = align_temporal_states(X_est, X_true, r) if align else X_est
+    return float(((Xa.astype(np.float64) - X_true) ** 2).mean()), Xa
+
+
+def correlation_after_alignment(X_est, X_true, r):
+    """alignment.py:414-436."""
+    _, Xa = compute_alignment_error(X_est, X_true, r)
+    a = Xa.astype(np.float64).ravel()
+    b = X_true.astype(np.float64).ravel()
+    a = a - a.mean()
+    b = b - b.mean()
+    den = np.sqrt((a * a).sum() * (b * b).sum())
+    return 0.0 if den < 1e-10 else float((a * b).sum() / den)

@@ -48,7 +48,8 @@ class ame_elbo_args(ctypes.Structure):
 # every symbol include/ame_amd.h declares (checked by tests/test_capi.py)
 EXPORTS = ("ame_pack_y", "ame_sweep", "ame_sweep_work_size", "ame_sweep_orders_slices", "ame_sweep_max_slices", "ame_sweep_lds_bytes", "ame_cov",
            "ame_elbo", "ame_elbo_work_size", "ame_host_register", "ame_host_unregister",
-           "ame_supported_r", "ame_last_error", "ame_version")
+           "ame_supported_r", "ame_last_error", "ame_version", "ame_align_work_size",
+           "ame_align_cross_size", "ame_align_partials_size", "ame_align_cross", "ame_align_apply")
 
 _lock = threading.Lock()
 _lib = None
@@ -74,6 +75,17 @@ def _declare(L):
     L.ame_supported_r.argtypes = [P(ctypes.c_int), ctypes.c_int]
     L.ame_host_register.argtypes = [c_vp, ctypes.c_ulonglong, P(c_vp)]
     L.ame_host_unregister.argtypes = [c_vp]
+    ci = ctypes.c_int
+    for name in ("ame_align_work_size", "ame_align_cross_size"):
+        getattr(L, name).restype = ctypes.c_longlong
+    L.ame_align_work_size.argtypes = [ci, ci, ci]
+    L.ame_align_cross_size.argtypes = [ci, ci, ci, ci]
+    L.ame_align_partials_size.argtypes = [ci, ci]
+    L.ame_align_partials_size.restype = ctypes.c_longlong
+    L.ame_align_cross.argtypes = [c_vp, c_vp, ci, ci, ci, ci, c_vp, c_vp, c_vp]
+    L.ame_align_cross.restype = ci
+    L.ame_align_apply.argtypes = [c_vp, c_vp, ci, ci, ci, ci, c_vp, c_vp, c_vp, c_vp]
+    L.ame_align_apply.restype = ci
     L.ame_last_error.restype = ctypes.c_char_p
     L.ame_version.restype = ctypes.c_char_p
     for name in ("ame_pack_y", "ame_sweep", "ame_cov", "ame_elbo", "ame_sweep_max_slices",

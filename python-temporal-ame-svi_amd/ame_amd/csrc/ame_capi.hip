@@ -16,6 +16,11 @@ long long ame_sweep3_work_doubles(const ame_dims*);
 int ame_cov_dispatch(const ame_dims*, const ame_cov_args*, hipStream_t);
 int ame_elbo_dispatch(const ame_dims*, const ame_elbo_args*, hipStream_t);
 long long ame_elbo_work_doubles(const ame_dims*);
+int ame_align_cross_dispatch(const float*, const float*, int, int, int, int, double*, double*,
+                             hipStream_t);
+int ame_align_apply_dispatch(const float*, const float*, int, int, int, int, const double*, float*,
+                             double*, hipStream_t);
+long long ame_align_partials_count(int n, int T);
 int ame_pack_dispatch(const float*, float*, const ame_dims*, unsigned long long*, hipStream_t);
 
 static thread_local char g_err[512] = "";
@@ -168,6 +173,43 @@ int ame_elbo(const ame_dims* dims, const ame_elbo_args* a, void* stream) {
     if (dims->t_begin > 0 && !a->prev_final)
         return fail("ame_elbo: t_begin=%d > 0 needs prev_final", dims->t_begin);
     return launched(ame_elbo_dispatch(dims, a, (hipStream_t)stream), "elbo");
+}
+
+static int check_align(int n, int T, int r) {
+    if (n < 1 || T < 1) return fail("ame_align: bad n=%d T=%d", n, T);
+    if (!r_supported(r)) return fail("ame_align: latent_dim r=%d not compiled into this library", r);
+    return 0;
+}
+
+long long ame_align_work_size(int n, int T, int r) {
+    if (check_align(n, T, r)) return -1;
+    return 2LL * n * 2 * r;
+}
+
+long long ame_align_cross_size(int n, int T, int r, int global_mode) {
+    if (check_align(n, T, r)) return -1;
+    return global_mode ? 4LL * r * r : 2LL * T * r * r;
+}
+
+long long ame_align_partials_size(int n, int T) {
+    if (n < 1 || T < 1) return fail("ame_align: bad n=%d T=%d", n, T);
+    return ame_align_partials_count(n, T);
+}
+
+int ame_align_cross(const float* x_est, const float* x_true, int n, int T, int r, int global_mode,
+                    double* cross, double* work, void* stream) {
+    if (int e = check_align(n, T, r)) return e;
+    if (!x_est || !x_true || !cross || (global_mode && !work)) return fail("ame_align_cross: NULL buffer");
+    return launched(ame_align_cross_dispatch(x_est, x_true, n, T, r, global_mode, cross, work,
+                                             (hipStream_t)stream), "align_cross");
+}
+
+int ame_align_apply(const float* x_est, const float* x_true, int n, int T, int r, int global_mode,
+                    const double* rot, float* x_out, double* partials, void* stream) {
+    if (int e = check_align(n, T, r)) return e;
+    if (!x_est || !x_true || !rot || !x_out || !partials) return fail("ame_align_apply: NULL buffer");
+    return launched(ame_align_apply_dispatch(x_est, x_true, n, T, r, global_mode, rot, x_out,
+                                             partials, (hipStream_t)stream), "align_apply");
 }
 
 }  // extern "C"

@@ -18,7 +18,7 @@ BDIR = os.path.join(PKG, "ame_amd", "_build")
 TAG = ([a.split("=", 1)[1] for a in sys.argv if a.startswith("--tag=")] or [""])[0]
 SO = os.path.join(BDIR, f"libame_amd_stamps3{TAG}.so")
 SRCS = ("ame_sweep.hip", "ame_sweep3.hip", "ame_cov.hip", "ame_elbo.hip", "ame_capi.hip",
-        "ame_selftest.hip")
+        "ame_selftest.hip", "ame_align.hip")
 NAMES = {
     0: ["start", "J+kj", "reduce", "ddone", "2x2+assembly", "publish", "kcnt", "brow"],
     1: ["start", "-", "poll", "hf1", "HB", "GEMV", "-", "-", "-", "end"],
