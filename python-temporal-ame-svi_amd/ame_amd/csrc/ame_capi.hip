@@ -122,9 +122,16 @@ int ame_sweep_max_slices(int n, int r) {
 
 int ame_sweep_orders_slices(int n, int r) { return r_supported(r) && use_v3(n, r) ? 1 : 0; }
 
+// v2 with the slice's (U,V) block in HBM: [T_local][n][2r] fp32 in the work buffer
+static long long v2_global_doubles(const ame_dims* d) {
+    if (use_v3(d->n, d->r) || !sweep_lds_layout(d->n, d->r, ame_sweep_force_global()).m_global) return 0;
+    return ((long long)d->T_local * d->n * 2 * d->r + 1) / 2;
+}
+
 long long ame_sweep_work_size(const ame_dims* dims) {
     if (check_dims(dims)) return -1;
-    return ame_sweep3_work_doubles(dims);
+    const long long a = ame_sweep3_work_doubles(dims), b = v2_global_doubles(dims);
+    return a > b ? a : b;
 }
 
 int ame_pack_y(const float* Y, float* Yt, const ame_dims* dims, unsigned long long* mismatch,
@@ -146,6 +153,8 @@ int ame_sweep(const ame_dims* dims, const ame_sweep_args* a, void* stream) {
     const bool v3 = use_v3(dims->n, dims->r);
     if (!v3 && sweep_lds_layout(dims->n, dims->r, ame_sweep_force_global()).total > AME_LDS_MAX)
         return fail("ame_sweep: slice state (n=%d, r=%d) exceeds one workgroup's LDS", dims->n, dims->r);
+    if (v2_global_doubles(dims) > 0 && !a->work)
+        return fail("ame_sweep: n=%d, r=%d keeps the slice in HBM and needs the work buffer", dims->n, dims->r);
     if (a->wait_epoch != 0 && (!v3 || !a->done))
         return fail("ame_sweep: wait_epoch needs the v3 sweep and a done array");
     const int maxs = ame_sweep_max_slices(dims->n, dims->r);

@@ -134,11 +134,13 @@ __device__ __forceinline__ void tri_decode(int e, int& k, int& m) {
     m = e - k * (k + 1) / 2;
 }
 
-// MG = false: the slice's (U,V) block lives in LDS (M).  MG = true: it is read
-// from the mean buffers (xn for nodes < split, i.e. already updated in this
-// sweep, xo from split on); wave 0 drains its mean stores (vmcnt(0)) before
-// the barrier that precedes the next GEMV, the workgroup-scope release of the
-// AMDGPU memory model (one CU, shared vL1D).
+// MG = false: the slice's (U,V) block lives in LDS (M).  MG = true: it lives in
+// a compact HBM copy (a.work, [T_local][n][2R] fp32, 16-byte aligned rows)
+// that wave 0 updates when it publishes a new mean; wave 0 drains its stores
+// (vmcnt(0)) before the barrier that precedes the next GEMV, the
+// workgroup-scope release of the AMDGPU memory model (one CU, shared vL1D).
+// Old values the step itself needs (node i-1 in phase 1, node i in phase 3)
+// come from x_old in that mode.
 template <int R, bool MG>
 __global__ void __launch_bounds__(AME_NT)
 ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
@@ -191,27 +193,32 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     const float* ysl = a.Yt + (size_t)tl * n * n * 2;
     const float lr = a.lr, om = a.one_minus_lr;
     bool dead = false;
-    // (U,V) row of node j: new for j < split (this sweep), old from split on
-    auto mrow = [&](int j, int split) -> const float* {
-        if constexpr (MG) return (j < split ? (const float*)xn : xo) + (size_t)j * D + 2;
+    float* Mg = MG ? (float*)a.work + (size_t)tl * n * M2 : nullptr;
+    // (U,V) row of node j as the GEMV sees it (new for nodes already published)
+    auto mrow = [&](int j) -> const float* {
+        if constexpr (MG) return Mg + (size_t)j * M2;
+        else return M + j * M2;
+    };
+    // OLD (U,V) row of node j
+    auto mold = [&](int j) -> const float* {
+        if constexpr (MG) return xo + (size_t)j * D + 2;
         else return M + j * M2;
     };
 
     // ------------------------------------------------------------------
     // init: slice state, P_0 = P_const + sum_{j != 0} F_j, K_0 = P_0^-1
     // ------------------------------------------------------------------
-    if constexpr (!MG) {
-        for (int idx = tid; idx < n * M2; idx += AME_NT) {
-            const int j = idx / M2, c = idx - j * M2;
-            M[idx] = xo[(size_t)j * D + 2 + c];
-        }
+    for (int idx = tid; idx < n * M2; idx += AME_NT) {
+        const int j = idx / M2, c = idx - j * M2;
+        if constexpr (MG) Mg[idx] = xo[(size_t)j * D + 2 + c];
+        else M[idx] = xo[(size_t)j * D + 2 + c];
     }
     if (tid < D) pcd[tid] = pconst_entry(a.consts, D, tid, tid, tg, Tt);
     __syncthreads();
     if (tid < M2) {   // sum of squares over all nodes: ssq[c<R] = sum U_c^2, ssq[R+c] = sum V_c^2
         double acc = 0.0;
         for (int j = 0; j < n; ++j) {
-            const double v = (double)mrow(j, 0)[tid];
+            const double v = (double)mold(j)[tid];
             acc = fma(v, v, acc);
         }
         ssq[tid] = acc;
@@ -228,14 +235,14 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             const int kc = ku ? R + ck : ck - R;
             double acc = 0.0;
             if (m < 2) {
-                for (int j = 1; j < n; ++j) acc += (double)mrow(j, 0)[kc];
+                for (int j = 1; j < n; ++j) acc += (double)mold(j)[kc];
                 v = (ku ? (m == 0 ? p : q) : (m == 0 ? q : s)) * acc;
             } else {
                 const int cm = m - 2;
                 const bool mu_ = cm < R;
                 const int mc = mu_ ? R + cm : cm - R;
                 for (int j = 1; j < n; ++j)
-                    acc = fma((double)mrow(j, 0)[kc], (double)mrow(j, 0)[mc], acc);
+                    acc = fma((double)mold(j)[kc], (double)mold(j)[mc], acc);
                 v = ((ku && mu_) ? p : ((!ku && !mu_) ? s : q)) * acc;
             }
         }
@@ -320,7 +327,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         const float2* yrow = (const float2*)(ysl + (size_t)node * n * 2);
         for (int j = tid + AME_NT * AME_YPF; j < n; j += AME_NT) put(j, yrow[j]);
     };
-    auto gemv = [&](int tw, int split) {   // partial h_obs over node group (waves 1-3: tw < 192)
+    auto gemv = [&](int tw) {   // partial h_obs over node group (waves 1-3: tw < 192)
         const int g = tw / CW, cq = tw - g * CW;
         if (g < GW) {
             const int c0 = cq * VEC;
@@ -330,18 +337,13 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
 #pragma unroll
             for (int v = 0; v < VEC; ++v) acc[v] = 0.f;
             float s0 = 0.f, s1 = 0.f;
-#pragma unroll 4
+            // HBM rows (MG): more loads in flight per thread
+#pragma unroll (MG ? 8 : 4)
             for (int j = g; j < n; j += GW) {
                 const float2 zz = z[j];
                 const float zc = upart ? zz.x : zz.y;
-                const float* mr = mrow(j, split) + mo;
-                if constexpr (MG && VEC == 4) {   // rows are 8-byte aligned in HBM
-                    const float2 m0 = *(const float2*)mr, m1 = *(const float2*)(mr + 2);
-                    acc[0] = fmaf(zc, m0.x, acc[0]);
-                    acc[1] = fmaf(zc, m0.y, acc[1]);
-                    acc[2] = fmaf(zc, m1.x, acc[2]);
-                    acc[3] = fmaf(zc, m1.y, acc[3]);
-                } else if constexpr (VEC == 4) {
+                const float* mr = mrow(j) + mo;
+                if constexpr (VEC == 4) {
                     const float4 mv = *(const float4*)mr;
                     acc[0] = fmaf(zc, mv.x, acc[0]);
                     acc[1] = fmaf(zc, mv.y, acc[1]);
@@ -477,7 +479,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     }
     if (n > 1) prefetch_y(1);
     __syncthreads();
-    if (wave >= 1) gemv(tid - 64, 0);
+    if (wave >= 1) gemv(tid - 64);
     __syncthreads();
     gemv_reduce();
     ar_terms();
@@ -505,7 +507,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         }
         // ---------------- phase 1 ----------------
         if (has_prev && tid < M2) {   // node i-1: statistics and slice (U,V) <- new
-            const double vo = (double)mrow(i - 1, i - 1)[tid], vn = (double)mu_prev[2 + tid];
+            const double vo = (double)mold(i - 1)[tid], vn = (double)mu_prev[2 + tid];
             ssq[tid] = ssq[tid] - vo * vo + vn * vn;
             if constexpr (!MG) M[(i - 1) * M2 + tid] = mu_prev[2 + tid];
         }
@@ -521,7 +523,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                     const bool prevv = qv < 2;
                     if (prevv ? has_prev : has_next) {
                         const bool row0 = (qv & 1) == 0;   // e0 = [1,0,V,0] ; e1 = [0,1,0,U]
-                        const float* src = prevv ? (mu_prev + 2) : mrow(i + 1, i + 1);
+                        const float* src = prevv ? (mu_prev + 2) : mrow(i + 1);
                         const int cb = row0 ? 2 : 2 + R;
                         const float* vv = row0 ? (src + R) : src;
                         acc = K[k * KS + (row0 ? 0 : 1)];
@@ -547,7 +549,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             if (has_next) stage_z(i + 1, i);
             STAMPW(7, 0);
         }
-        // MG: node i-1's new mean (xn, stored by wave 0 in the previous step) is
+        // MG: node i-1's (U,V) row (stored by wave 0 in the previous step) is
         // read by this step's GEMV in waves 1-3: drain it before the barrier
         if constexpr (MG) {
             if (wave == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -559,7 +561,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             // lane owns state rows k = lane + 64h (h < KH)
             double W0[KH], W1[KH], Y0[KH], Y1[KH], ua[KH], uM[KH], gk[KH], K0[KH], K1[KH];
             double jp0[KH], jp1[KH], jn0[KH], jn1[KH];
-            const float* mnext = has_next ? mrow(i + 1, i + 1) : nullptr;
+            const float* mnext = has_next ? mrow(i + 1) : nullptr;
 #pragma unroll
             for (int h = 0; h < KH; ++h) {
                 const int k = lane + 64 * h;
@@ -655,6 +657,9 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 if (k < D) {   // damped new mean; publish (mu_prev: readers above are done, wave-ordered)
                     const float nw = __fadd_rn(__fmul_rn(lr, (float)mus[h]), __fmul_rn(om, mu_old[k]));
                     xn[(size_t)i * D + k] = nw;
+                    if constexpr (MG) {
+                        if (k >= 2) Mg[(size_t)i * M2 + (k - 2)] = nw;
+                    }
                     mu_prev[k] = nw;
                     const uint64_t g = ((uint64_t)a.epoch << 32) | (uint64_t)__float_as_uint(nw);
                     gran_store_agent(a.hand + ((size_t)tl * n + i) * D + k, g);
@@ -703,7 +708,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             uint64_t g0[KH];
             if (wave == 1) first_poll(i + 1, g0);
             if (i + 2 < n) prefetch_y(i + 2);
-            gemv(tid - 64, i);
+            gemv(tid - 64);
             STAMPW(11, 64);
             STAMPW(13, 128);
             if (wave == 1) {
@@ -738,10 +743,10 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                         if (k == 0) pd = p * (double)(n - 1);
                         else if (k == 1) pd = s * (double)(n - 1);
                         else if (k < 2 + R) {
-                            const double vo = (double)mrow(i, i)[R + (k - 2)];
+                            const double vo = (double)mold(i)[R + (k - 2)];
                             pd = p * (ssq[R + (k - 2)] - vo * vo);
                         } else {
-                            const double uo = (double)mrow(i, i)[k - 2 - R];
+                            const double uo = (double)mold(i)[k - 2 - R];
                             pd = s * (ssq[k - 2 - R] - uo * uo);
                         }
                         c32 = 1.0f / ((float)(pd + pcd[k]) + 1e-8f);
