@@ -4,8 +4,8 @@ One engine per process / GPU.  It owns, for the local time slices
 [t_begin, t_begin + T_local):
 
     Yt        [T_local][n][n][2] fp32   observed network, time-major (ame_pack_y)
-    x_a, x_b  [T_local][n][d]    fp32   means: current state / spare
-    cov, cov_b[T_local][n][d][d] fp32   covariances: current state / spare
+    xs[k]     [T_local][n][d]    fp32   means: ring of spec_depth + 1 states
+    covs[k]   [T_local][n][d][d] fp32   covariances: same ring (x_a / cov = current)
     hand      [T_local][n][d]    u64    lane-to-lane {epoch,value} granules
     cov_terms [T_local][n][4]    fp64   per-(node,time) covariance ELBO terms
 
@@ -34,6 +34,7 @@ the kernels in order (tests/test_gpu_parity.py::test_speculative_sweep_is_exact)
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 import math
 import os
@@ -153,10 +154,10 @@ class DeviceEngine:
             self.phi = self.C.Phi.contiguous().to(dev)
             self._pack_y(model.Y)
             t0, t1 = sh.t_begin, sh.t_begin + sh.T_local
-            self.x_a = X_mean[:, t0:t1].detach().float().permute(1, 0, 2).contiguous().to(dev)
-            self.x_b = torch.empty_like(self.x_a)
-            self.cov = X_cov[:, t0:t1].detach().float().permute(1, 0, 2, 3).contiguous().to(dev)
-            self.cov_b = torch.empty_like(self.cov)
+            x0 = X_mean[:, t0:t1].detach().float().permute(1, 0, 2).contiguous().to(dev)
+            c0 = X_cov[:, t0:t1].detach().float().permute(1, 0, 2, 3).contiguous().to(dev)
+            self.xs, self.covs = [x0], [c0]
+            self._cur = 0
             n, d, TL = self.n, self.d, sh.T_local
             self.hand = torch.zeros(TL * n * d, dtype=torch.int64, device=dev)
             self.cov_terms = torch.zeros(TL * n * 4, dtype=torch.float64, device=dev)
@@ -181,7 +182,7 @@ class DeviceEngine:
         self.timing = False       # record HIP events around each kernel launch
         self.events = []          # (name, start, end) while timing
         self.speculation = os.environ.get("AME_SPECULATE", "1") != "0"
-        self._spec = None         # done-event of a sweep started ahead of its update_step
+        self._specs = collections.deque()   # (done-event, ring slot) of sweeps started ahead
         # consecutive sweeps alternate between two high-priority streams
         self.sweep_streams = [torch.cuda.Stream(device=self.dev, priority=-1) for _ in range(2)]
         self.done = torch.zeros(max(sh.T_local, 1), dtype=torch.int32, device=self.dev)
@@ -190,6 +191,27 @@ class DeviceEngine:
                           and os.environ.get("AME_PIPELINE", "1") != "0")
         if self.halo is not None:   # every rank must take the same path
             self.pipelined = self.halo.agree(self, self.pipelined)
+        # How many sweeps may run ahead of the committed state.  Pipelined sweeps
+        # overlap slice by slice, so a deeper queue keeps the wavefront full when
+        # its fill over all T slices (all ranks) exceeds one iteration: the host
+        # reads iteration k's ELBO only after sweep k has finished everywhere, and
+        # sweep k+depth must already be queued by then.
+        self.spec_depth = int(os.environ.get("AME_SPEC_DEPTH", "2" if self.pipelined else "1"))
+        if self.spec_depth < 1:
+            raise ValueError("AME_SPEC_DEPTH must be >= 1")
+        with torch.cuda.device(dev):
+            while len(self.xs) < self.spec_depth + 1:
+                self.xs.append(torch.empty_like(self.xs[0]))
+                self.covs.append(torch.empty_like(self.covs[0]))
+
+    # current state (ring slot _cur)
+    @property
+    def x_a(self) -> torch.Tensor:
+        return self.xs[self._cur]
+
+    @property
+    def cov(self) -> torch.Tensor:
+        return self.covs[self._cur]
 
     # ------------------------------------------------------------------
     def _sp(self):
@@ -236,11 +258,19 @@ class DeviceEngine:
 
     # ------------------------------------------------------------------
     def _launch_sweep(self, spec=False):
-        """Enqueue one sweep (x_a, cov) -> (x_b, cov_b); returns its done-event.
+        """Enqueue one sweep from the newest state (the last queued sweep's
+        output, or the current state) into the next ring slot; returns
+        (done-event, slot).
         A speculative sweep in pipelined mode is queued while the previous sweep
         (epoch - 1) still runs and orders itself slice by slice on the device;
         any other sweep is ordered after everything queued on the main stream."""
+        src = self._specs[-1][1] if self._specs else self._cur
+        dst = (src + 1) % len(self.xs)
         self.epoch += 1
+        # two streams: sweep k+2 queues behind sweep k's local slices, which keeps
+        # the launch-order XCD placement of its workgroups (three streams, measured:
+        # 16 % slower per iteration at n=128); the host-side constraint a deeper
+        # queue lifts is global (DESIGN.md §5)
         stream = self.sweep_streams[self.epoch & 1]
         pipe = spec and self.pipelined and self.speculation
         halo_in = halo_out = next_old = back_in = back_out = None
@@ -257,11 +287,11 @@ class DeviceEngine:
             ready.record(self.stream)
             stream.wait_event(ready)
         a = _lib.ame_sweep_args(
-            Yt=_ptr(self.Yt), x_old=_ptr(self.x_a), x_new=_ptr(self.x_b), next_old=next_old,
-            hand=_ptr(self.hand), halo_in=halo_in, halo_out=halo_out, cov=_ptr(self.cov),
+            Yt=_ptr(self.Yt), x_old=_ptr(self.xs[src]), x_new=_ptr(self.xs[dst]), next_old=next_old,
+            hand=_ptr(self.hand), halo_in=halo_in, halo_out=halo_out, cov=_ptr(self.covs[src]),
             consts=_ptr(self.consts), rinv=self.C.rinv4(), lr=self.lr,
             one_minus_lr=float(1.0 - self.lr), epoch=self.epoch, status=_ptr(self.status),
-            work=_ptr(self.sweep_work), cov_new=_ptr(self.cov_b), done=_ptr(self.done),
+            work=_ptr(self.sweep_work), cov_new=_ptr(self.covs[dst]), done=_ptr(self.done),
             wait_epoch=wait, back_out=back_out, back_in=back_in)
         tok = self._tic("sweep", stream)
         _lib.check(self.L.ame_sweep(ctypes.byref(self.dims), ctypes.byref(a),
@@ -269,38 +299,42 @@ class DeviceEngine:
         self._toc(tok)
         done = torch.cuda.Event()
         done.record(stream)
-        return done
+        return done, dst
 
-    def _swap(self):
-        self.x_a, self.x_b = self.x_b, self.x_a
-        self.cov, self.cov_b = self.cov_b, self.cov
+    def _commit(self, slot):
+        self._cur = slot
         self._out_valid = False
         self._cov_terms_valid = False
 
     def sweep(self):
         """One Gauss-Seidel sweep + covariance update (reference _update_step).
         A sweep already started from this state (speculate) is only committed."""
-        if self._spec is not None:
-            done, self._spec = self._spec, None
+        if self._specs:
+            done, slot = self._specs.popleft()
         else:
-            done = self._launch_sweep()
+            done, slot = self._launch_sweep()
         self.stream.wait_event(done)
-        self._swap()
+        self._commit(slot)
         if self.halo is not None:
             self.halo.after_sweep(self)
 
-    def speculate(self):
-        """Start the next sweep now, from the current state, on the sweep stream."""
-        if self._spec is not None or not self.speculation:
+    def speculate(self, ahead=1):
+        """Keep min(ahead, spec_depth) sweeps started beyond the current state.
+        Each reads the previous one's output ring slot; none touches the current
+        state, and the oldest slot it overwrites belongs to a state whose ELBO
+        the host has already read."""
+        if not self.speculation:
             return
-        self._spec = self._launch_sweep(spec=True)
+        want = min(int(ahead), self.spec_depth)
+        while len(self._specs) < want:
+            self._specs.append(self._launch_sweep(spec=True))
 
     def discard_speculation(self):
-        """Drop a started sweep that will not be committed.  It writes only the
-        spare buffers; later main-stream work is ordered after it."""
-        if self._spec is not None:
-            self.stream.wait_event(self._spec)
-            self._spec = None
+        """Drop started sweeps that will not be committed.  They write only
+        spare ring slots; later main-stream work is ordered after them."""
+        while self._specs:
+            done, _ = self._specs.popleft()
+            self.stream.wait_event(done)
 
     def refresh_cov_terms(self):
         """Covariance ELBO terms of the current covariances (no update)."""
@@ -327,12 +361,13 @@ class DeviceEngine:
                    "ame_elbo")
         self._toc(tok)
 
-    def sums(self, speculate=False):
+    def sums(self, speculate=0):
         """The 8 fp64 sums for the current state (all ranks reduced).  With
-        speculate=True the next sweep is started first and runs beside them."""
+        speculate=k > 0 (iterations still to come) up to k next sweeps are
+        started first and run beside them."""
         if not self._out_valid:
             if speculate:
-                self.speculate()
+                self.speculate(int(speculate))
             self.launch_elbo()
             out = self.out
             if self.halo is not None:
@@ -342,7 +377,7 @@ class DeviceEngine:
             self._out_valid = True
         return self._out_host
 
-    def terms(self, speculate=False):
+    def terms(self, speculate=0):
         return assemble(self.sums(speculate), self.n, self.T, self.d, self.variant, self.C)
 
     def _check_status(self):

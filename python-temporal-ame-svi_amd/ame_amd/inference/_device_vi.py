@@ -124,16 +124,17 @@ class DeviceTemporalVI(BaseTemporalVariationalInference):
 
     # ---------------- fit() hooks: the speculation window ----------------
     def _fit_iteration(self, iteration: int, max_iter: int) -> None:
-        # another iteration follows this one unless fit() converges first
-        self._spec_next = iteration < max_iter - 1
+        # iterations that follow this one unless fit() converges first: that many
+        # sweeps may be started ahead (bounded by the engine's spec_depth)
+        self._spec_next = max(0, max_iter - 1 - iteration)
 
     def _fit_end(self) -> None:
-        self._spec_next = False
+        self._spec_next = 0
         if self._engine is not None:
             self._engine.discard_speculation()
 
     def _terms(self):
-        return self._ensure_engine().terms(speculate=getattr(self, "_spec_next", False))
+        return self._ensure_engine().terms(speculate=getattr(self, "_spec_next", 0))
 
     def _compute_elbo(self):
         # the reference returns a 0-d fp32 tensor (python float + fp32 tensors)

@@ -243,3 +243,23 @@ def test_pipelined_sweeps_many_slices(gpu_device):
     assert np.array_equal(a.X_mean.numpy(), b.X_mean.numpy())
     assert np.array_equal(a.X_cov.numpy(), b.X_cov.numpy())
     assert [float(e) for e in ha["elbo"]] == [float(e) for e in hb["elbo"]]
+
+
+@pytest.mark.parametrize("depth", ["1", "3"])
+def test_speculation_depth_is_exact(depth, gpu_device, monkeypatch):
+    """Sweeps queued `depth` deep (state ring of depth + 1 slots, each slice
+    waiting on the device for the previous sweep): bit-identical to the
+    in-order schedule, also when fit() stops at convergence with sweeps still
+    queued, and when a later fit() continues."""
+    monkeypatch.setenv("AME_SPEC_DEPTH", depth)
+    a, b = _twins(90, 40, 4, "good", 0.5, gpu_device)
+    assert a.engine.spec_depth == int(depth) and len(a.engine.xs) == int(depth) + 1
+    ha = a.fit(max_iter=7, tolerance=0.0, verbose=False)
+    hb = b.fit(max_iter=7, tolerance=0.0, verbose=False)
+    assert [float(e) for e in ha["elbo"]] == [float(e) for e in hb["elbo"]]
+    for vi in (a, b):
+        vi.fit(max_iter=10, tolerance=1.0, verbose=False)   # stops at its 4th iteration
+        vi.fit(max_iter=2, tolerance=0.0, verbose=False)
+    assert np.array_equal(a.X_mean.numpy(), b.X_mean.numpy())
+    assert np.array_equal(a.X_cov.numpy(), b.X_cov.numpy())
+    assert [float(e) for e in a.history["elbo"]] == [float(e) for e in b.history["elbo"]]
