@@ -1,6 +1,8 @@
-"""Time-sharded sweep on the GPU: 2 ranks (processes) on one MI355X, boundary
-means handed over through the host-mapped granule buffer while both sweep
-kernels run.  Must reproduce the single-process result bit for bit (means,
+"""Time-sharded sweep on the GPU: 2-4 ranks (processes) on one MI355X, boundary
+means handed over through the host-mapped granule buffers while the ranks'
+sweep kernels run (with 3+ ranks a middle rank has both neighbours: left halo
+in, right halo out and both back channels at once; 6 iterations keep sweeps
+queued two deep across ranks).  Must reproduce the single-process result bit for bit (means,
 covariances) and the ELBO/MSE to fp64 round-off."""
 import os
 import socket
@@ -48,16 +50,17 @@ def _worker(rank, world, port, args, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n,T,r,method,lr", [(64, 8, 4, "good", 0.5), (40, 6, 3, "bad", 1.0),
-                                             (48, 5, 2, "naive", 0.3)])
-def test_two_ranks_one_gpu(n, T, r, method, lr):
+@pytest.mark.parametrize("world,n,T,r,method,lr,iters", [
+    (2, 64, 8, 4, "good", 0.5, 3), (2, 40, 6, 3, "bad", 1.0, 3), (2, 48, 5, 2, "naive", 0.3, 3),
+    (3, 50, 9, 3, "good", 0.5, 6), (4, 40, 12, 4, "good", 0.7, 6)])
+def test_ranks_one_gpu(world, n, T, r, method, lr, iters):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    args = (n, T, r, method, lr, 3)
+    args = (n, T, r, method, lr, iters)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(rk, 2, port, args, q)) for rk in range(2)]
+    procs = [ctx.Process(target=_worker, args=(rk, world, port, args, q)) for rk in range(world)]
     for p in procs:
         p.start()
     try:
@@ -71,7 +74,7 @@ def test_two_ranks_one_gpu(n, T, r, method, lr):
         if p.exitcode is None:
             p.kill()
             p.join()
-    assert codes == [0, 0], f"rank exit codes {codes}"
+    assert codes == [0] * world, f"rank exit codes {codes}"
     mean_d, cov_d, elbo_d, rec_d = result
     mean_s, cov_s, elbo_s, rec_s = _run(*args, distributed=False)
     assert np.array_equal(mean_d, mean_s)
