@@ -30,35 +30,46 @@ class TemporalAMEStructuredMFVI(DeviceTemporalVI):
         self._variant = factorization
         super().__init__(model, learning_rate, seed, device=device, distributed=distributed)
 
+    # (node, time) blocks per chunk of the covariance init: the arithmetic runs
+    # chunk by chunk into the preallocated X_cov, so host memory stays at one
+    # X_cov (4.8 GB at n=1024, T=1024, r=16) instead of several full temporaries
+    _INIT_CHUNK = 8192
+
     def _initialize_variational_params(self) -> None:
         """structured_mf.py:74-113: identical random stream (one randn(n,T,d),
         then one randn per block per (i,t), in loop order); the elementwise
-        arithmetic is batched, which is bit-identical in fp32."""
+        arithmetic is batched per chunk, which is bit-identical in fp32."""
         n, T, d, r = self.n, self.T, self.d, self.r
         self.X_mean = torch.randn(n, T, d) * self.init_scale
+        N, K = n * T, self._INIT_CHUNK
         if self.factorization == "good":
-            E = torch.stack([torch.randn(d, d) for _ in range(n * T)]).view(n, T, d, d)
+            out = torch.empty(N, d, d)
             eye = torch.eye(d)
-            cov = eye * self.cov_init_scale
-            cov = cov + E * 0.01
-            cov = (cov + cov.transpose(-1, -2)) / 2
-            cov = cov + eye * 0.1
-            self.X_cov = cov.contiguous()
+            for k0 in range(0, N, K):
+                k1 = min(N, k0 + K)
+                E = torch.stack([torch.randn(d, d) for _ in range(k1 - k0)])
+                cov = eye * self.cov_init_scale
+                cov = cov + E * 0.01
+                cov = (cov + cov.transpose(-1, -2)) / 2
+                out[k0:k1] = cov + eye * 0.1
+            self.X_cov = out.view(n, T, d, d)
         elif self.factorization == "bad":
             r2 = 2 * r
-            E1 = torch.empty(n * T, 2, 2)
-            E2 = torch.empty(n * T, r2, r2)
-            for k in range(n * T):
-                E1[k] = torch.randn(2, 2)
-                E2[k] = torch.randn(r2, r2)
-            b1 = torch.eye(2) * self.cov_init_scale + E1 * 0.01
-            b1 = (b1 + b1.transpose(-1, -2)) / 2 + torch.eye(2) * 0.05
-            b2 = torch.eye(r2) * self.cov_init_scale + E2 * 0.01
-            b2 = (b2 + b2.transpose(-1, -2)) / 2 + torch.eye(r2) * 0.05
-            cov = torch.zeros(n * T, d, d)
-            cov[:, :2, :2] = b1
-            cov[:, 2:, 2:] = b2
-            self.X_cov = cov.view(n, T, d, d).contiguous()
+            out = torch.zeros(N, d, d)
+            for k0 in range(0, N, K):
+                k1 = min(N, k0 + K)
+                E1 = torch.empty(k1 - k0, 2, 2)
+                E2 = torch.empty(k1 - k0, r2, r2)
+                for k in range(k1 - k0):
+                    E1[k] = torch.randn(2, 2)
+                    E2[k] = torch.randn(r2, r2)
+                b1 = torch.eye(2) * self.cov_init_scale + E1 * 0.01
+                b1 = (b1 + b1.transpose(-1, -2)) / 2 + torch.eye(2) * 0.05
+                b2 = torch.eye(r2) * self.cov_init_scale + E2 * 0.01
+                b2 = (b2 + b2.transpose(-1, -2)) / 2 + torch.eye(r2) * 0.05
+                out[k0:k1, :2, :2] = b1
+                out[k0:k1, 2:, 2:] = b2
+            self.X_cov = out.view(n, T, d, d)
         else:
             self.X_cov = torch.zeros(n, T, d, d)
             raise ValueError(f"Unknown factorization '{self.factorization}'")
