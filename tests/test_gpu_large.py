@@ -83,6 +83,15 @@ def test_v2_lds_slice_vs_oracle(n, T, r, method, lr, gpu_device, monkeypatch):
     _check_vs_oracle(n, T, r, method, lr, gpu_device)
 
 
+def test_auto_global_slice_past_v3(gpu_device):
+    """n = 3400, r = 16: past the v3 sweep's register/LDS budget and past the v2
+    LDS slice, so the v2 sweep keeps the slice in HBM on its own."""
+    from ame_amd import _lib
+    L = _lib.lib()
+    assert L.ame_sweep_orders_slices(3400, 16) == 0          # not the v3 sweep
+    _check_vs_oracle(3400, 1, 16, "good", 0.5, gpu_device, iters=1)
+
+
 @pytest.mark.parametrize("method", ["good", "bad", "naive"])
 def test_config5_shape_prefix_and_elbo(method, gpu_device):
     """n = 4096, r = 32 (config 5), 3 slices: the first 3 nodes of one sweep

@@ -122,7 +122,9 @@ def test_single_node_update(gpu_device):
     (33, 7, 1, "good", 0.5), (64, 16, 4, "good", 0.01), (50, 9, 5, "bad", 1.0),
     (48, 6, 8, "naive", 0.3), (70, 5, 6, "good", 1.0), (40, 4, 16, "good", 0.01),
     (20, 1, 2, "good", 1.0), (2, 3, 2, "bad", 0.7), (24, 3, 7, "naive", 1.0),
-    (1000, 2, 16, "good", 0.5), (700, 3, 8, "naive", 1.0), (900, 2, 16, "bad", 0.2)])
+    (1000, 2, 16, "good", 0.5), (700, 3, 8, "naive", 1.0), (900, 2, 16, "bad", 0.2),
+    (60, 3, 12, "good", 0.5), (50, 3, 24, "bad", 0.7), (30, 2, 24, "naive", 1.0),
+    (1200, 1, 24, "good", 0.3)])
 def test_vs_oracle_fp64(n, T, r, method, lr, gpu_device):
     """Random configurations (odd r, T=1, n=2, ...) against the fp64 oracle.
 
