@@ -84,8 +84,10 @@ typedef struct ame_sweep_args {
     float one_minus_lr;          /* (float)(1 - lr) computed in double on the host */
     uint32_t epoch;              /* sweep counter, >= 1, identical on every rank */
     uint32_t* status;            /* [1] error word */
-    double* work;                /* scratch, >= ame_sweep_work_size() doubles (per-slice base
-                                    inverse and column sums of squares) */
+    double* work;                /* scratch, >= ame_sweep_work_size() doubles: 0 for the v3
+                                    sweep; [T_local][n][2r] fp32 (U,V) copy when the v2 sweep
+                                    keeps the slice in HBM (n = 4096, r = 32, ...); may be NULL
+                                    when the size is 0 */
     float* cov_new;              /* [T_local][n][d][d] damped covariances after the sweep, or NULL
                                     (in place).  A separate buffer lets ame_cov / ame_elbo read
                                     `cov` while the next sweep already runs (engine speculation) */
@@ -137,7 +139,7 @@ int ame_sweep(const ame_dims* dims, const ame_sweep_args* args, void* stream);
 /* 1 when ame_sweep for (n, r) honours done / wait_epoch, else 0. */
 int ame_sweep_orders_slices(int n, int r);
 
-/* Scratch doubles ame_sweep needs in args->work. */
+/* Scratch doubles ame_sweep needs in args->work (see the field). */
 long long ame_sweep_work_size(const ame_dims* dims);
 
 /* Largest T_local ame_sweep can run with for (n, r) on this device, 0 if the
