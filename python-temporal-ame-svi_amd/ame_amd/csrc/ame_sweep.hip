@@ -65,6 +65,9 @@ extern "C" int ame_debug_read_stamps(unsigned long long* host, int count) {
 #endif
 
 #define AME_YPF 8   // Y-row prefetch registers per thread (n <= 2048 fully prefetched)
+#ifndef AME_MG_UNROLL
+#define AME_MG_UNROLL 8   // GEMV rows in flight per thread when the slice is read from HBM
+#endif
 
 // Workgroup barrier that orders LDS only.  __syncthreads() lowers to a release
 // fence that waits vmcnt(0), exposing every in-flight prefetch load and every
@@ -338,7 +341,8 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             for (int v = 0; v < VEC; ++v) acc[v] = 0.f;
             float s0 = 0.f, s1 = 0.f;
             // HBM rows (MG): more loads in flight per thread
-#pragma unroll (MG ? 8 : 4)
+            constexpr int kUnroll = MG ? AME_MG_UNROLL : 4;
+#pragma unroll kUnroll
             for (int j = g; j < n; j += GW) {
                 const float2 zz = z[j];
                 const float zc = upart ? zz.x : zz.y;
