@@ -1,7 +1,7 @@
 """Diagnostic: per-phase cycle shares of one sweep step (in-kernel s_memtime stamps).
 
-    python tools/sweep_stamps.py --build      # here: hipcc -DAME_STAMPS -> _build/libame_amd_stamps.so
-    python tools/sweep_stamps.py              # GPU box: config-3 sweep, print phase shares
+    python tools/sweep_stamps.py --build [--r=16]          # here: hipcc -DAME_STAMPS -> _build/libame_amd_stamps.so
+    python tools/sweep_stamps.py [--n=1024 --T=128 --r=16] # GPU box: v2 sweep (AME_SWEEP_V2=1), phase shares
 
 Stamps are taken by thread 0 of the middle lane for 16 nodes in steady state.
 The stamped build's run time is never quoted; only its SHARES are meaningful.
@@ -34,7 +34,8 @@ def build(r=16):
     tag = _opt("--tag", "")
     so = SO.replace(".so", f"{tag}.so")
     objs = []
-    for src in ("ame_sweep.hip", "ame_cov.hip", "ame_elbo.hip", "ame_capi.hip"):
+    for src in ("ame_sweep.hip", "ame_sweep3.hip", "ame_cov.hip", "ame_elbo.hip", "ame_capi.hip",
+                "ame_selftest.hip", "ame_align.hip"):
         o = os.path.join(BDIR, src.replace(".hip", f"_stamps{tag}.o"))
         subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17",
                                "-DAME_STAMPS", f"-DAME_ONLY_R={r}", *defs, "-Wno-pass-failed",
@@ -46,12 +47,14 @@ def build(r=16):
 
 def run():
     os.environ["AME_LIB_PATH"] = SO.replace(".so", f"{_opt('--tag', '')}.so")
+    os.environ["AME_SWEEP_V2"] = "1"
+    n, T, r = int(_opt("--n", 1024)), int(_opt("--T", 128)), int(_opt("--r", 16))
     sys.path.insert(0, PKG)
     import torch
     from ame_amd import TemporalAMEModel, TemporalAMEStructuredMFVI
     from ame_amd import _lib
     dev = torch.device("cuda", 0)
-    m = TemporalAMEModel(1024, 128, 16, seed=42)
+    m = TemporalAMEModel(n, T, r, seed=42)
     m.generate_data_fast(device=dev)
     vi = TemporalAMEStructuredMFVI(m, factorization="good", learning_rate=0.01, device=dev)
     vi.fit(max_iter=2, tolerance=0.0, verbose=False)
@@ -86,4 +89,4 @@ def run():
 
 
 if __name__ == "__main__":
-    build() if "--build" in sys.argv else run()
+    build(int(_opt("--r", 16))) if "--build" in sys.argv else run()
