@@ -216,6 +216,8 @@ def main():
                                   "the sweep is latency-bound (n dependent steps per slice)")
                          if getattr(eng, "pipelined", False) else None},
             "kernels_ms": kms,
+            "schedule": {"pipelined": bool(getattr(eng, "pipelined", False)),
+                         "sweeps_queued_ahead": int(getattr(eng, "spec_depth", 1))},
             "iteration_roofline_frac": b_iter / (dt / args.steps) / (world * HBM_PEAK_GBS * 1e9),
             "cpu_baseline": cpu,
             "elbo_last": elbo_last,
