@@ -45,3 +45,25 @@ def test_alignment_kernel_path_needs_gpu():
     X = torch.zeros(4, 2, 6)
     with pytest.raises(RuntimeError):
         align_temporal_states(X, X, 2)
+
+
+def test_run_method_with_timing_contract(capsys):
+    """experiments/utils.py:146-229 result keys and prints, on a host-only VI
+    stand-in (the device engine's kernel times are added when it has one)."""
+    from ame_amd.utils import run_method_with_timing
+
+    class FakeVI:
+        def __init__(self, model, learning_rate=1.0):
+            self.model, self.lr = model, learning_rate
+            self.X_mean = torch.ones(2, 3, 4)
+
+        def fit(self, max_iter=100, verbose=True):
+            return {"elbo": [torch.tensor(-3.0)] * max_iter,
+                    "reconstruction_error": [0.5] * max_iter}
+
+    res = run_method_with_timing(FakeVI, object(), "Fake", max_iter=4, learning_rate=0.1)
+    assert res["iterations"] == 4 and res["method_name"] == "Fake"
+    assert res["vi"].lr == 0.1 and torch.equal(res["X_est"], torch.ones(2, 3, 4))
+    assert res["runtime"] >= 0 and "kernels_ms" not in res
+    out = capsys.readouterr().out
+    assert "Running: Fake" in out and "Final MSE: 0.500000" in out
