@@ -48,23 +48,43 @@ def kernel_bytes(n, TL, d, swap_consistent=True):
     }
 
 
-def cpu_baseline(model, vi, n, T, d, budget_s=20.0):
-    """Time the numpy oracle (fp32, reference dtype) on a bounded sample of the
-    same iteration and extrapolate linearly to one full iteration."""
+def _host_info():
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:  # pragma: no cover
+        pass
+    return {"host_cpus": os.cpu_count(), "cpu_model": model}
+
+
+def cpu_baseline(model, vi, n, T, d, budget_s=24.0):
+    """Time the CPU restatements (fp32, the reference's dtype) on bounded
+    samples of the same iteration and extrapolate to one full iteration.
+
+    * main value: the vectorised numpy oracle (oracle/ame_oracle.py; BLAS
+      threads = the threads numpy uses on this host), SURVEY.md §8d(ii);
+    * ``loop_restatement``: oracle/ame_loop_oracle.py, the reference's cost
+      model (one small torch op sequence per ordered dyad / unordered pair,
+      structured_mf.py:130-148, :303-324), SURVEY.md §8d(i).
+    """
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ame_oracle as O
+    import ame_loop_oracle as LO
     try:
         from threadpoolctl import threadpool_info
-        cores = max([p.get("num_threads", 1) for p in threadpool_info()] + [1])
+        threads = max([p.get("num_threads", 1) for p in threadpool_info()] + [1])
     except Exception:  # pragma: no cover
-        cores = 1
+        threads = 1
     Y = model.Y.detach().cpu().numpy().astype(np.float32)
     Xm = vi.X_mean.numpy().astype(np.float32).copy()
     Xc = vi.X_cov.numpy().astype(np.float32).copy()
     params = {k: getattr(model, k).detach().cpu().numpy().astype(np.float32)
               for k in ("R", "R_inv", "Sigma", "Psi", "Phi", "Q")}
     consts = O.prior_terms(params, T, np.float32)
-    # calibrate on one node
+    # --- vectorised oracle: a block of nodes of the sweep ---
     t0 = time.perf_counter()
     O.update_node(Y, Xm, Xc, params, 0, "good", 0.01, consts)
     per_node = time.perf_counter() - t0
@@ -72,9 +92,12 @@ def cpu_baseline(model, vi, n, T, d, budget_s=20.0):
     t0 = time.perf_counter()
     for i in range(1, 1 + k):
         O.update_node(Y, Xm, Xc, params, i, "good", 0.01, consts)
-    t_nodes = time.perf_counter() - t0
-    sweep_est = t_nodes / k * n
-    m = max(1, min(T, 4))
+    sweep_est = (time.perf_counter() - t0) / k * n
+    # loglik + MSE on a set of whole slices
+    t0 = time.perf_counter()
+    O.expected_loglik(Y, Xm, Xc, params, "good", ts=range(1))
+    per_slice = time.perf_counter() - t0
+    m = int(max(1, min(T, (0.25 * budget_s) / max(2.0 * per_slice, 1e-6))))
     t0 = time.perf_counter()
     O.expected_loglik(Y, Xm, Xc, params, "good", ts=range(m))
     t_ll = (time.perf_counter() - t0) / m * T
@@ -84,7 +107,7 @@ def cpu_baseline(model, vi, n, T, d, budget_s=20.0):
         mu = O.compute_mean(Xm[:, t].astype(np.float64), (d - 2) // 2)
         float((((Y[:, :, t] - mu) ** 2)[off]).sum())
     t_rec = (time.perf_counter() - t0) / m * T
-    kn = min(n, 32)
+    kn = min(n, 64)
     t0 = time.perf_counter()
     O.entropy(Xc[:kn])
     O.log_prior_transitions(Xm[:kn], Xc[:kn], params)
@@ -92,13 +115,63 @@ def cpu_baseline(model, vi, n, T, d, budget_s=20.0):
     t_node_terms = (time.perf_counter() - t0) / kn * n
     it_est = sweep_est + t_ll + t_rec + t_node_terms
     units = T * n * (n - 1) / 2.0
+    # --- loop-structured restatement: exact-size sample of update steps and pairs ---
+    Yt = torch.from_numpy(Y)
+    Xm_t, Xc_t = torch.from_numpy(Xm), torch.from_numpy(Xc)
+    lb = 0.15 * budget_s
+    t0 = time.perf_counter()
+    LO.update_node_loop(Yt, Xm_t, Xc_t, params, n - 1, "good", 0.01, ts=range(1))
+    per_step = time.perf_counter() - t0
+    ns = int(max(1, min(T - 1, lb / max(per_step, 1e-6))))
+    t0 = time.perf_counter()
+    LO.update_node_loop(Yt, Xm_t, Xc_t, params, n - 1, "good", 0.01, ts=range(1, 1 + ns))
+    per_step = (time.perf_counter() - t0) / ns
+    rng = np.random.default_rng(0)
+    npairs = 2000
+    t0 = time.perf_counter()
+    sample = [(int(a), int(b)) for a, b in (sorted(rng.choice(n, 2, replace=False))
+                                            for _ in range(npairs))]
+    LO.loglik_pairs_loop(Yt, Xm_t, Xc_t, params, "good", 0, pairs=sample[:200])
+    per_pair = (time.perf_counter() - t0) / 200
+    npairs = int(max(200, min(200000, lb / max(per_pair, 1e-9))))
+    sample = [(int(a), int(b)) for a, b in (sorted(rng.choice(n, 2, replace=False))
+                                            for _ in range(npairs))]
+    t0 = time.perf_counter()
+    LO.loglik_pairs_loop(Yt, Xm_t, Xc_t, params, "good", 0, pairs=sample)
+    per_pair = (time.perf_counter() - t0) / npairs
+    loop_it = per_step * n * T + per_pair * units + t_rec + t_node_terms
     return {
-        "value": units / it_est, "unit": UNIT, "cores": int(cores), "kind": "port",
-        "sample": (f"numpy oracle fp32 on this host: update_node for {k + 1} of {n} nodes x {T} "
-                   f"slices, loglik+MSE for {m} of {T} slices, entropy/prior terms for {kn} "
-                   f"nodes; extrapolated linearly to one full iteration "
-                   f"(est. {it_est:.1f} s/iteration)"),
+        "value": units / it_est, "unit": UNIT, "cores": int(threads), "kind": "port",
+        "sample": (f"numpy oracle (oracle/ame_oracle.py) fp32, {threads} BLAS threads: "
+                   f"update_node for {k + 1} of {n} nodes x {T} slices, loglik+MSE for {m} of "
+                   f"{T} slices, entropy/prior terms for {kn} nodes; extrapolated linearly to "
+                   f"one full iteration (est. {it_est:.1f} s/iteration)"),
+        **_host_info(),
+        "loop_restatement": {
+            "value": units / loop_it, "unit": UNIT, "cores": 1, "kind": "port",
+            "sample": (f"oracle/ame_loop_oracle.py (reference cost model: a torch op sequence "
+                       f"per ordered dyad / unordered pair, fp32): {ns} (node, t) update steps "
+                       f"at n={n} ({per_step * 1e3:.1f} ms each), {npairs} loglik pairs "
+                       f"({per_pair * 1e6:.1f} us each); extrapolated to one iteration "
+                       f"(est. {loop_it / 3600:.2f} h/iteration)"),
+        },
     }
+
+
+def isolated_ms(eng, reps=5):
+    """Average ms of the covariance-terms and ELBO launches alone on the GPU
+    (no sweep beside them), HIP events recorded on the stream they run on."""
+    eng.events.clear()
+    eng.timing = True
+    torch.cuda.synchronize(eng.dev)
+    for _ in range(reps):
+        eng.refresh_cov_terms()
+        eng.launch_elbo()
+        torch.cuda.synchronize(eng.dev)
+    ms, _ = eng.kernel_ms()
+    eng.timing = False
+    eng.invalidate()
+    return ms
 
 
 def load_pmc(tag):
@@ -125,7 +198,7 @@ def main():
     ap.add_argument("--variant", default="good", choices=["good", "bad", "naive"])
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--cpu-budget", type=float, default=24.0)
     args = ap.parse_args()
 
     import torch.distributed as dist
@@ -177,18 +250,38 @@ def main():
     kms, kcount = eng.kernel_ms()
     TL = eng.shard.T_local
     kb = kernel_bytes(n, TL, d, eng.swap_consistent)
-    dom = max(kms, key=kms.get)
-    achieved = kb[dom] / (kms[dom] * 1e-3) / 1e9
     units_per_step = T_total * n * (n - 1) / 2.0
     value = units_per_step * args.steps / dt
     ms_step = dt / args.steps * 1e3
     b_iter = 8.0 * n * (n - 1) * T_total + 4.0 * n * (n - 1) * T_total \
         + 12.0 * n * T_total * d * d + 16.0 * n * T_total * d
     tag = f"n{n}_T{args.t_per_gpu}_r{r}_{args.variant}"
-    pmc = load_pmc(tag)
-    traffic = None
-    if pmc is not None and dom in pmc.get("kernels", {}):
-        traffic = pmc["kernels"][dom].get("hbm_bytes_per_launch")
+    pmc = (load_pmc(tag) or {}).get("kernels", {})
+    # cov / elbo launches once more, alone on the GPU (after the timed region)
+    iso = isolated_ms(eng)
+    pipelined = bool(getattr(eng, "pipelined", False))
+    kernels = {}
+    for name, ms, how in (
+            ("sweep", ms_step, "per-iteration time (one sweep retires per fit() iteration; "
+                               "pipelined launches overlap, so a launch's own duration is not "
+                               "a per-sweep figure)"),
+            ("cov", iso.get("cov"), "isolated launch, HIP events on its stream"),
+            ("elbo", iso.get("elbo"), "isolated launch (pair + node + final kernels), HIP "
+                                      "events on its stream")):
+        ent = {"alg_bytes": kb[name], "ms": ms, "timing": how,
+               "launch_ms_in_fit": kms.get(name)}
+        if ms:
+            ach = kb[name] / (ms * 1e-3) / 1e9
+            ent.update(achieved_GBs=ach, frac=ach / HBM_PEAK_GBS)
+        pk = pmc.get({"elbo": "pairs"}.get(name, name))
+        if pk:
+            ent["traffic"] = pk.get("hbm_bytes_per_launch")
+            ent["traffic_kernel"] = pk.get("kernel")
+            if ent["traffic"]:
+                alg = kb[name] if name != "elbo" else pk.get("alg_bytes", kb[name])
+                ent["traffic_over_alg"] = ent["traffic"] / alg
+        kernels[name] = ent
+    sw = kernels["sweep"]
 
     out = None
     if rank == 0:
@@ -196,27 +289,34 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(model, vi, n, T_total, d, budget_s=args.cpu_budget)
         elbo_last = float(hist["elbo"][-1])
+        shape = (n, args.t_per_gpu, r)
+        named = {(1024, 128, 16): "BASELINE config 3 shape per GPU",
+                 (256, 64, 8): "BASELINE config 2 shape per GPU",
+                 (1024, 64, 16): "BASELINE config 4 per-rank shape (T=512 over 8 GPUs)",
+                 (4096, 32, 32): "BASELINE config 5 per-rank shape (T=256 over 8 GPUs)"}
+        label = named.get(shape, "custom shape")
         out = {
             "metric": METRIC, "value": value, "unit": UNIT, "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f32", "data": "synthetic",
             "config": {
-                "workload": (f"BASELINE config 3 shape per GPU: n_nodes={n}, n_time={args.t_per_gpu}"
-                             f"/GPU (T_total={T_total}), latent_dim={r} (d={d}), "
+                "workload": (f"{label}: n_nodes={n}, n_time={args.t_per_gpu}/GPU "
+                             f"(T_total={T_total}), latent_dim={r} (d={d}), "
                              f"SMF-{args.variant} fit iteration, lr={args.lr}"),
                 "n_nodes": n, "n_time_total": T_total, "latent_dim": r, "d": d,
                 "variant": args.variant, "parallelism": f"time-sharded x{world}",
             },
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic,
-                         "note": ("sweep launches are pipelined: a launch starts while the "
-                                  "previous sweep runs and its duration includes that wait; "
-                                  "the sweep is latency-bound (n dependent steps per slice)")
-                         if getattr(eng, "pipelined", False) else None},
-            "kernels_ms": kms,
-            "schedule": {"pipelined": bool(getattr(eng, "pipelined", False)),
+            "roofline": {"bound": "hbm", "kernel": "sweep", "achieved": sw["achieved_GBs"],
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": sw["frac"],
+                         "traffic": sw.get("traffic"),
+                         "note": ("achieved = the sweep's algorithmic bytes per launch "
+                                  "(DESIGN.md §4) / ms_per_step: one sweep retires per "
+                                  "iteration" + ("; launches are pipelined" if pipelined else "")
+                                  + ". The sweep is latency-bound: n dependent node steps "
+                                  "per slice")},
+            "kernels": kernels,
+            "schedule": {"pipelined": pipelined,
                          "sweeps_queued_ahead": int(getattr(eng, "spec_depth", 1))},
             "iteration_roofline_frac": b_iter / (dt / args.steps) / (world * HBM_PEAK_GBS * 1e9),
             "cpu_baseline": cpu,

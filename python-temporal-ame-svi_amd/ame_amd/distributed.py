@@ -169,12 +169,14 @@ class TimeShardHalo:
             back_out = ctypes.c_void_p(self.left.dev.value + self._back_off)
         return back_in, back_out
 
-    def before_sweep(self, eng, gather=True):
+    def before_sweep(self, eng, gather=True, first=None):
+        """first: this rank's first slice of the sweep's input state (the
+        current state unless given)."""
         self._setup(eng)
         rank, world = self.shard.rank, self.shard.world
         next_old = None
         if gather:
-            firsts = self._all_gather_slice(eng.x_a[0])
+            firsts = self._all_gather_slice(eng.x_a[0] if first is None else first)
             if rank < world - 1:
                 self._next_old = firsts[rank + 1]
                 next_old = ctypes.c_void_p(self._next_old.data_ptr())

@@ -199,6 +199,12 @@ class DeviceEngine:
         self.spec_depth = int(os.environ.get("AME_SPEC_DEPTH", "2" if self.pipelined else "1"))
         if self.spec_depth < 1:
             raise ValueError("AME_SPEC_DEPTH must be >= 1")
+        if not self.pipelined:
+            # A sweep that does not order itself slice by slice on the device must
+            # not start before the sweep that writes its input slot has finished;
+            # with more than one queued that is a serial chain anyway, so the
+            # queue is one deep (_launch_sweep also orders after the last one).
+            self.spec_depth = 1
         with torch.cuda.device(dev):
             while len(self.xs) < self.spec_depth + 1:
                 self.xs.append(torch.empty_like(self.xs[0]))
@@ -277,7 +283,8 @@ class DeviceEngine:
         if self.halo is not None:
             # a pipelined launch takes next_old from the back channel instead of a
             # collective that would wait for the running sweep
-            next_old, halo_in, halo_out = self.halo.before_sweep(self, gather=not pipe)
+            next_old, halo_in, halo_out = self.halo.before_sweep(
+                self, gather=not pipe, first=self.xs[src][0])
             back_in, back_out = self.halo.back_channels(self)
         wait = 0
         if pipe:
@@ -286,6 +293,8 @@ class DeviceEngine:
             ready = torch.cuda.Event()
             ready.record(self.stream)
             stream.wait_event(ready)
+            if self._specs:   # its input slot is the output of the last queued sweep
+                stream.wait_event(self._specs[-1][0])
         a = _lib.ame_sweep_args(
             Yt=_ptr(self.Yt), x_old=_ptr(self.xs[src]), x_new=_ptr(self.xs[dst]), next_old=next_old,
             hand=_ptr(self.hand), halo_in=halo_in, halo_out=halo_out, cov=_ptr(self.covs[src]),

@@ -2,10 +2,18 @@
 (``X_mean (n,T,d)``, ``X_cov (n,T,d,d)``, CPU fp32) are lazily synchronised views.
 
 Synchronisation rule: after a device step the device copy is authoritative;
-reading ``vi.X_mean`` downloads it once and remembers the tensor's version
-counter.  Assigning ``vi.X_mean = ...`` or mutating the downloaded tensor in
-place (which bumps ``tensor._version``) makes the host copy authoritative again
-and it is uploaded before the next device step.
+reading ``vi.X_mean`` downloads it once, INTO the host tensor handed out
+before (so a reference a caller kept, ``X = vi.X_mean``, sees the fitted
+values once the attribute has been read again, like the reference's live
+tensor), and remembers the tensor's version counter.  Assigning
+``vi.X_mean = ...`` or mutating the host tensor in place (which bumps
+``tensor._version``) makes the host copy authoritative again and it is
+uploaded before the next device step.
+
+Time-sharded runs: reading ``X_mean`` / ``X_cov`` after a device step is a
+COLLECTIVE (every rank's slices are all-gathered), so every rank must read
+it, e.g. not only ``if rank == 0``.  ``local_means()`` / ``local_covs()``
+return this rank's own slices without communication.
 """
 from __future__ import annotations
 
@@ -47,6 +55,13 @@ class DeviceTemporalVI(BaseTemporalVariationalInference):
                 t = self._gather(eng.means_local(), axis=1)
             else:
                 t = self._gather(eng.covs_local(), axis=1)
+            h = self._host[key]
+            if h is not None and h.shape == t.shape and h.dtype == t.dtype and not h.is_inference():
+                # refresh in place: a tensor a caller took earlier (X = vi.X_mean)
+                # sees the update, as the reference's live attribute does
+                # (structured_mf.py:282-287, 332-338)
+                h.copy_(t)
+                t = h
             self._host[key] = t
             self._ver[key] = t._version
             self._stale[key] = False
@@ -158,6 +173,15 @@ class DeviceTemporalVI(BaseTemporalVariationalInference):
     def elbo_terms(self) -> dict:
         """fp64 ELBO pieces + MSE of the current state (extension)."""
         return dict(self._terms())
+
+    def local_means(self) -> torch.Tensor:
+        """This rank's slices (n, T_local, d) of the current means, on the CPU,
+        without a collective (extension; equals X_mean on one process)."""
+        return self._ensure_engine().means_local().detach().to("cpu").contiguous()
+
+    def local_covs(self) -> torch.Tensor:
+        """This rank's slices (n, T_local, d, d) of the current covariances."""
+        return self._ensure_engine().covs_local().detach().to("cpu").contiguous()
 
     def get_variational_means(self) -> torch.Tensor:
         return self.X_mean

@@ -91,7 +91,9 @@ def _align_device(X_est: torch.Tensor, X_true: torch.Tensor, r: int,
                                      ctypes.c_void_p(out.data_ptr()),
                                      ctypes.c_void_p(part.data_ptr()), sp), "ame_align_apply")
         sq = float(part.sum().item())
-    return out.to(X_est.device), sq
+    # the kernels compute in fp32; hand back the caller's dtype and device
+    # (the reference returns X_est-typed results, alignment.py:275-321)
+    return out.to(X_est.device, X_est.dtype), sq
 
 
 def procrustes_alignment(X_est: torch.Tensor, X_true: torch.Tensor,

@@ -38,6 +38,22 @@ def test_align_vs_reference(tag, gpu_device):
         assert abs(c - z[f"{name}_corr"]) <= 1e-5
 
 
+def test_align_keeps_fp64_dtype(gpu_device):
+    """fp64 inputs come back fp64 (the kernels compute in fp32; the reference
+    returns X_est-typed results, alignment.py:275-321)."""
+    from ame_amd.utils import align_latent_positions, align_temporal_states
+    z = golden("c1_align.npz")
+    r = int(z["r"])
+    Xt = torch.from_numpy(z["X_true"]).double()
+    name = [k[:-4] for k in z.files if k.endswith("_est")][0]
+    Xe = torch.from_numpy(z[f"{name}_est"]).double()
+    each = align_temporal_states(Xe, Xt, r)
+    assert each.dtype == torch.float64 and each.device == Xe.device
+    assert np.abs(each.numpy() - z[f"{name}_each"]).max() <= 2e-5 * max(1.0, float(Xt.abs().max()))
+    lat = align_latent_positions(Xe[:, 0, 2:], Xt[:, 0, 2:], r)
+    assert lat.dtype == torch.float64
+
+
 @pytest.mark.parametrize("n,T,r", [(1024, 16, 16), (500, 6, 32), (77, 3, 1)])
 def test_align_vs_oracle_large(n, T, r, gpu_device):
     """Device-resident inputs at config sizes against the fp64 oracle."""

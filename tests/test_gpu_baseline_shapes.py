@@ -1,0 +1,186 @@
+"""GPU parity at the BASELINE.json configuration shapes, through the C-ABI.
+
+* config 2 (n=256, T=64, r=8): the whole fit (2 iterations, good / bad /
+  naive) against the fp64 oracle;
+* config 3 (n=1024, T=128, r=16, lr=0.01 -- the bench workload): the
+  production schedule (speculative, pipelined sweeps queued two deep) is bit
+  for bit the in-order schedule, and the in-order run's third sweep is checked
+  on its first K nodes of all 128 slices against the oracle replaying that
+  sweep prefix from the device's state after two iterations (node i depends
+  only on the pre-sweep state and on nodes < i: SURVEY.md App. B); the device
+  ELBO / MSE of the full state against the oracle's ELBO of the same state;
+* config 4's per-rank shape (n=1024, T_local=64, r=16): two time-sharded
+  ranks on one GPU reproduce the single-process T=128 run bit for bit.
+
+Reference: structured_mf.py:211-326 (sweep), :115-209 (ELBO),
+naive_mf.py:207-282, temporal_ame.py:255-291 (MSE).
+
+Tolerances as in test_gpu_parity.py: means within 5e-6 * max(1, |mu|) of the
+fp64 oracle or no further from it than the reference's own fp32 arithmetic
+(the fp32 oracle) is; covariances 1e-6 * max(1, |S|); ELBO / MSE 5e-6 relative.
+"""
+import hashlib
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+PKEYS = ("R", "R_inv", "Sigma", "Psi", "Phi", "Q")
+
+
+def _vi(model, method, lr, dev, distributed=None):
+    from ame_amd import TemporalAMENaiveMFVI, TemporalAMEStructuredMFVI
+    if method == "naive":
+        return TemporalAMENaiveMFVI(model, learning_rate=lr, device=dev, distributed=distributed)
+    return TemporalAMEStructuredMFVI(model, factorization=method, learning_rate=lr, device=dev,
+                                     distributed=distributed)
+
+
+def _params(m, dtype=np.float64):
+    return {k: getattr(m, k).cpu().numpy().astype(dtype) for k in PKEYS}
+
+
+@pytest.mark.parametrize("method", ["good", "bad", "naive"])
+def test_config2_full_fit(method, gpu_device):
+    """BASELINE config 2 at full size: 2 fit iterations vs the fp64 oracle."""
+    import ame_oracle as O
+    from ame_amd import TemporalAMEModel
+    n, T, r, lr = 256, 64, 8, 0.01
+    m = TemporalAMEModel(n, T, r, seed=42)
+    m.generate_data_fast(seed=42)
+    vi = _vi(m, method, lr, gpu_device)
+    Xm = vi.X_mean.numpy().astype(np.float64).copy()
+    Xc = vi.X_cov.numpy().astype(np.float64).copy()
+    Xm32, Xc32 = vi.X_mean.numpy().copy(), vi.X_cov.numpy().copy()
+    ref = O.fit(m.Y.numpy().astype(np.float64), Xm, Xc, _params(m), method, lr, 2, 0.0)
+    O.fit(m.Y.numpy(), Xm32, Xc32, _params(m, np.float32), method, lr, 2, 0.0)
+    fp32_err = np.abs(Xm32.astype(np.float64) - Xm).max()
+    h = vi.fit(max_iter=2, tolerance=0.0, verbose=False)
+    err = np.abs(vi.X_mean.numpy() - Xm).max()
+    assert err <= max(5e-6 * max(1.0, np.abs(Xm).max()), fp32_err), (err, fp32_err)
+    cerr = np.abs(vi.X_cov.numpy() - Xc).max()
+    assert cerr <= 1e-6 * max(1.0, np.abs(Xc).max()), cerr
+    for a, b in zip(h["elbo"], ref["elbo"]):
+        assert abs(float(a) - b) <= 5e-6 * abs(b), (float(a), b)
+    for a, b in zip(h["reconstruction_error"], ref["reconstruction_error"]):
+        assert abs(a - b) <= 5e-6 * abs(b), (a, b)
+
+
+def _config3(dev):
+    from ame_amd import TemporalAMEModel
+    m = TemporalAMEModel(1024, 128, 16, seed=42)
+    m.generate_data_fast(device=dev, seed=42)
+    return m
+
+
+def test_config3_schedule_prefix_and_elbo(gpu_device):
+    """BASELINE config 3 (the bench workload) at its own shape."""
+    import ame_oracle as O
+    n, T, r, lr, K = 1024, 128, 16, 0.01, 8
+    # production schedule: one fit() call, sweeps started ahead and pipelined
+    m = _config3(gpu_device)
+    prod = _vi(m, "good", lr, gpu_device)
+    assert prod.engine.pipelined and prod.engine.spec_depth == 2
+    hp = prod.fit(max_iter=3, tolerance=0.0, verbose=False)
+    prod_mean = prod.X_mean.numpy().copy()
+    prod_cov_digest = hashlib.sha256(prod.X_cov.numpy().tobytes()).hexdigest()
+    del prod
+    torch.cuda.empty_cache()
+    # in-order schedule, one iteration per fit() call, no speculation
+    m = _config3(gpu_device)
+    vi = _vi(m, "good", lr, gpu_device)
+    vi.engine.speculation = False
+    vi.fit(max_iter=2, tolerance=0.0, verbose=False)
+    Xm = vi.X_mean.numpy().astype(np.float64).copy()
+    Xc = vi.X_cov.numpy().astype(np.float64).copy()
+    Xm32, Xc32 = vi.X_mean.numpy().copy(), vi.X_cov.numpy().copy()
+    h = vi.fit(max_iter=1, tolerance=0.0, verbose=False)
+    got_m, got_c = vi.X_mean.numpy(), vi.X_cov.numpy()
+    # the pipelined schedule is the in-order one, bit for bit
+    assert np.array_equal(prod_mean, got_m)
+    assert prod_cov_digest == hashlib.sha256(got_c.tobytes()).hexdigest()
+    assert [float(e) for e in hp["elbo"]] == [float(e) for e in h["elbo"]]
+    assert hp["reconstruction_error"] == h["reconstruction_error"]
+    # sweep 3, nodes 0..K-1 of every slice, against the oracle's replay
+    Ycpu = m.Y.cpu().numpy()
+    Y64 = Ycpu.astype(np.float64)
+    p64, p32 = _params(m), _params(m, np.float32)
+    c64, c32 = O.prior_terms(p64, T, np.float64), O.prior_terms(p32, T, np.float32)
+    for i in range(K):
+        O.update_node(Y64, Xm, Xc, p64, i, "good", lr, c64)
+        O.update_node(Ycpu, Xm32, Xc32, p32, i, "good", lr, c32)
+    fp32_err = np.abs(Xm32[:K].astype(np.float64) - Xm[:K]).max()
+    err = np.abs(got_m[:K].astype(np.float64) - Xm[:K]).max()
+    assert err <= max(5e-6 * max(1.0, np.abs(Xm[:K]).max()), fp32_err), (err, fp32_err)
+    cerr = np.abs(got_c[:K].astype(np.float64) - Xc[:K]).max()
+    assert cerr <= 1e-6 * max(1.0, np.abs(Xc[:K]).max()), cerr
+    # the ELBO / MSE kernels on the full device state
+    e_ref = O.elbo(Y64, got_m, got_c, p64, "good")
+    mse_ref = O.recon_error(Y64, got_m)
+    assert abs(float(h["elbo"][-1]) - e_ref) <= 5e-6 * abs(e_ref), (float(h["elbo"][-1]), e_ref)
+    assert abs(h["reconstruction_error"][-1] - mse_ref) <= 5e-6 * mse_ref
+
+
+# ---------------- config 4 per-rank shape: 2 ranks x T_local=64 ----------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _c4_run(distributed):
+    dev = torch.device("cuda", 0)
+    m = _config3(dev)
+    vi = _vi(m, "good", 0.01, dev, distributed=distributed)
+    h = vi.fit(max_iter=3, tolerance=0.0, verbose=False)
+    mean = vi.X_mean.numpy().copy()
+    digest = hashlib.sha256(vi.X_cov.numpy().tobytes()).hexdigest()
+    return mean, digest, [float(e) for e in h["elbo"]], list(h["reconstruction_error"])
+
+
+def _c4_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = _c4_run(True)
+        if rank == 0:
+            q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_config4_rank_shape_two_ranks(gpu_device):
+    """n=1024, r=16, T=128 split over 2 ranks (T_local=64, config 4's per-rank
+    shape) on one GPU: bit-equal to the single-process run."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_c4_worker, args=(rk, 2, port, q)) for rk in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        result = q.get(timeout=110)
+    except Exception:
+        result = None
+    for p in procs:
+        p.join(timeout=30)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.exitcode is None:
+            p.kill()
+            p.join()
+    assert codes == [0, 0], f"rank exit codes {codes}"
+    mean_d, dig_d, elbo_d, rec_d = result
+    mean_s, dig_s, elbo_s, rec_s = _c4_run(False)
+    assert np.array_equal(mean_d, mean_s)
+    assert dig_d == dig_s
+    assert np.allclose(elbo_d, elbo_s, rtol=1e-6, atol=0)
+    assert np.allclose(rec_d, rec_s, rtol=1e-12, atol=0)

@@ -265,3 +265,36 @@ def test_speculation_depth_is_exact(depth, gpu_device, monkeypatch):
     assert np.array_equal(a.X_mean.numpy(), b.X_mean.numpy())
     assert np.array_equal(a.X_cov.numpy(), b.X_cov.numpy())
     assert [float(e) for e in a.history["elbo"]] == [float(e) for e in b.history["elbo"]]
+
+
+def test_unpipelined_queue_is_one_deep(gpu_device, monkeypatch):
+    """Sweeps that do not order themselves on the device (AME_PIPELINE=0) are
+    queued one deep whatever AME_SPEC_DEPTH asks, and stay exact."""
+    monkeypatch.setenv("AME_PIPELINE", "0")
+    monkeypatch.setenv("AME_SPEC_DEPTH", "2")
+    a, b = _twins(90, 40, 4, "good", 0.5, gpu_device)
+    assert not a.engine.pipelined and a.engine.spec_depth == 1
+    ha = a.fit(max_iter=5, tolerance=0.0, verbose=False)
+    hb = b.fit(max_iter=5, tolerance=0.0, verbose=False)
+    assert np.array_equal(a.X_mean.numpy(), b.X_mean.numpy())
+    assert np.array_equal(a.X_cov.numpy(), b.X_cov.numpy())
+    assert [float(e) for e in ha["elbo"]] == [float(e) for e in hb["elbo"]]
+
+
+def test_state_attributes_stay_live(gpu_device):
+    """X = vi.X_mean taken before fit() sees the fitted values once the
+    attribute is read again (reference getters return the live tensor,
+    structured_mf.py:328-338); a later host edit still goes to the device."""
+    from ame_amd import TemporalAMEModel
+    m = TemporalAMEModel(40, 6, 3, seed=9)
+    m.generate_data_fast(seed=9)
+    vi = _vi(m, "good", 0.5, gpu_device)
+    X, S = vi.X_mean, vi.X_cov
+    x0 = X.clone()
+    vi.fit(max_iter=2, tolerance=0.0, verbose=False)
+    assert vi.X_mean is X and vi.X_cov is S
+    assert not torch.equal(X, x0)
+    assert torch.equal(vi.get_variational_means(), X)
+    X[0, 0, 0] += 1.0                      # host edit -> uploaded before the next step
+    vi.fit(max_iter=1, tolerance=0.0, verbose=False)
+    assert vi.engine.x_a.shape[1] == 40

@@ -11,12 +11,12 @@ import os
 import sys
 
 
-def per_launch(outdir, sub, counter):
+def per_launch(outdir, sub, counter, kernel="ame_pairs_kernel"):
     vals = {}
     for f in glob.glob(os.path.join(outdir, sub, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if row["Counter_Name"] == counter:
+                if row["Counter_Name"] == counter and kernel in row["Kernel_Name"]:
                     k = row["Dispatch_Id"]
                     vals[k] = vals.get(k, 0.0) + float(row["Counter_Value"])
     if not vals:
@@ -27,7 +27,7 @@ def per_launch(outdir, sub, counter):
 
 def main():
     out = sys.argv[1]
-    fetch = per_launch(out, "pmc_pairs_fetch", "FETCH_SIZE")
+    fetch = per_launch(out, "pmc_FETCH_SIZE", "FETCH_SIZE")
     mfma = per_launch(out, "pmc_pairs_mfma", "SQ_VALU_MFMA_BUSY_CYCLES")
     gui = per_launch(out, "pmc_pairs_mfma", "GRBM_GUI_ACTIVE")
     cus = 256
