@@ -13,6 +13,10 @@ int ame_sweep3_dispatch(const ame_dims*, const ame_sweep_args*, hipStream_t);
 int ame_sweep3_supported(int n, int r);
 int ame_sweep3_blocks_per_cu(int n, int r);
 long long ame_sweep3_work_doubles(const ame_dims*);
+int ame_sweep4_dispatch(const ame_dims*, const ame_sweep_args*, hipStream_t);
+int ame_sweep4_supported(int n, int r);
+int ame_sweep4_blocks_per_cu(int n, int r);
+long long ame_sweep4_work_doubles(const ame_dims*);
 int ame_cov_dispatch(const ame_dims*, const ame_cov_args*, hipStream_t);
 int ame_elbo_dispatch(const ame_dims*, const ame_elbo_args*, hipStream_t);
 long long ame_elbo_work_doubles(const ame_dims*);
@@ -40,12 +44,23 @@ static bool r_supported(int r) {
     }
 }
 
-// v3 (solver + helper waves, register-resident slice) whenever the slice fits
-// its register budget; AME_SWEEP_V2=1 forces the v2 kernel (A/B runs).
+static bool env_on(const char* name) {
+    const char* e = getenv(name);
+    return e && e[0] && e[0] != '0';
+}
+// v3 (solver + helper waves, register-resident slice GEMV) when the slice fits
+// its register budget, else v2.  v4 (the observation term on MFMA block GEMMs
+// plus a window GEMV, r <= 16, n % 4 == 0, n <= 2048) is opt-in with
+// AME_SWEEP_V4=1: it is exact (tests/test_gpu_sweep4.py) but its step period
+// measured longer than v3's (profiles/r02_v4_*).  AME_SWEEP_V2=1
+// forces the v2 kernel (A/B runs, tests).
+static bool use_v4(int n, int r) {
+    if (env_on("AME_SWEEP_V2") || !env_on("AME_SWEEP_V4")) return false;
+    return ame_sweep4_supported(n, r) != 0;
+}
 static bool use_v3(int n, int r) {
-    const char* e = getenv("AME_SWEEP_V2");
-    if (e && e[0] && e[0] != '0') return false;
-    return ame_sweep3_supported(n, r) != 0;
+    if (env_on("AME_SWEEP_V2")) return false;
+    return use_v4(n, r) || ame_sweep3_supported(n, r) != 0;
 }
 
 static int check_dims(const ame_dims* d) {
@@ -116,7 +131,8 @@ int ame_sweep_max_slices(int n, int r) {
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    const int per_cu = v3 ? ame_sweep3_blocks_per_cu(n, r) : ame_sweep_blocks_per_cu(n, r);
+    const int per_cu = use_v4(n, r) ? ame_sweep4_blocks_per_cu(n, r)
+                       : v3 ? ame_sweep3_blocks_per_cu(n, r) : ame_sweep_blocks_per_cu(n, r);
     return per_cu * cus;
 }
 
@@ -130,6 +146,7 @@ static long long v2_global_doubles(const ame_dims* d) {
 
 long long ame_sweep_work_size(const ame_dims* dims) {
     if (check_dims(dims)) return -1;
+    if (use_v4(dims->n, dims->r)) return ame_sweep4_work_doubles(dims);
     const long long a = ame_sweep3_work_doubles(dims), b = v2_global_doubles(dims);
     return a > b ? a : b;
 }
@@ -153,13 +170,14 @@ int ame_sweep(const ame_dims* dims, const ame_sweep_args* a, void* stream) {
     const bool v3 = use_v3(dims->n, dims->r);
     if (!v3 && sweep_lds_layout(dims->n, dims->r, ame_sweep_force_global()).total > AME_LDS_MAX)
         return fail("ame_sweep: slice state (n=%d, r=%d) exceeds one workgroup's LDS", dims->n, dims->r);
-    if (v2_global_doubles(dims) > 0 && !a->work)
+    if ((v2_global_doubles(dims) > 0 || use_v4(dims->n, dims->r)) && !a->work)
         return fail("ame_sweep: n=%d, r=%d keeps the slice in HBM and needs the work buffer", dims->n, dims->r);
     if (a->wait_epoch != 0 && (!v3 || !a->done))
         return fail("ame_sweep: wait_epoch needs the v3 sweep and a done array");
     const int maxs = ame_sweep_max_slices(dims->n, dims->r);
     if (dims->T_local > maxs)
         return fail("ame_sweep: T_local=%d exceeds co-resident workgroups (%d)", dims->T_local, maxs);
+    if (use_v4(dims->n, dims->r)) return launched(ame_sweep4_dispatch(dims, a, (hipStream_t)stream), "sweep4");
     if (v3) return launched(ame_sweep3_dispatch(dims, a, (hipStream_t)stream), "sweep3");
     return launched(ame_sweep_dispatch(dims, a, (hipStream_t)stream), "sweep");
 }

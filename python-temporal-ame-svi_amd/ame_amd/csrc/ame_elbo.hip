@@ -57,7 +57,19 @@ int ame_pack_dispatch(const float* Y, float* Yt, const ame_dims* dm, unsigned lo
 }
 
 // ---------------------------------------------------------------------------
-// K2: pair terms.  work layout: [nwg2][2] = {sum quad (i<j), sum sq-err}
+// K2: pair terms.  work layout: [nwg][2] = {sum quad (i<j), sum sq-err}
+//
+// One workgroup walks whole 64-row strips of one slice: when Y is
+// swap-consistent, strip s and strip nb-1-s (the upper-triangle tiles J >= I
+// of both: nb + 1 tiles, so every workgroup gets the same work); otherwise one
+// strip over all nb tiles.  Wave w owns rows I0 + 16w .. +15 of the strip and
+// keeps U_I, V_I (its MFMA B operands) and a_I, b_I in registers for the whole
+// strip; the column tile's U_J, V_J, a_J, b_J are staged in LDS (double
+// buffered, one barrier per tile).  The products are formed transposed,
+//   G1^T = V_J U_I^T,  G2^T = U_J V_I^T   (v_mfma_f32_16x16x4_f32, exact f32),
+// so each lane's 4 accumulator values are 4 CONSECUTIVE columns j of one row i
+// and its Y values are one 32-byte run, loaded as two 16-byte loads issued for
+// the whole tile before the MFMAs.
 // ---------------------------------------------------------------------------
 #define AME_TILE 64
 
@@ -73,83 +85,116 @@ ame_pairs_kernel(ame_dims dm, const float* __restrict__ Yt, const float* __restr
     constexpr int LD = RP + 1;         // LDS row stride (bank spread)
     const int n = dm.n;
     const int nb = (n + AME_TILE - 1) / AME_TILE;
-    const int ntile = swap_mode ? nb * (nb + 1) / 2 : nb * nb;
-    const int tl = blockIdx.x / ntile;
-    int tix = blockIdx.x - tl * ntile;
-    int I, J;
-    if (swap_mode) {   // upper-triangle tile enumeration, row-major
-        I = 0;
-        while (tix >= nb - I) { tix -= nb - I; ++I; }
-        J = I + tix;
-    } else {
-        I = tix / nb;
-        J = tix - I * nb;
-    }
-    const int I0 = I * AME_TILE, J0 = J * AME_TILE;
+    const int nws = swap_mode ? (nb + 1) / 2 : nb;     // workgroups per slice
+    const int tl = blockIdx.x / nws;
+    const int s = blockIdx.x - tl * nws;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int li = lane & 15, lq = lane >> 4;
 
-    __shared__ float UI[AME_TILE * LD], VI[AME_TILE * LD], UJ[AME_TILE * LD], VJ[AME_TILE * LD];
-    __shared__ float aI[AME_TILE], bI[AME_TILE], aJ[AME_TILE], bJ[AME_TILE];
+    __shared__ float UJ[2][AME_TILE * LD], VJ[2][AME_TILE * LD];
+    __shared__ float aJ[2][AME_TILE], bJ[2][AME_TILE];
     __shared__ double red[8];
 
     const float* xs = x + (size_t)tl * n * D;
-    for (int idx = threadIdx.x; idx < AME_TILE * RP; idx += AME_NT) {
-        const int row = idx / RP, k = idx - row * RP;
-        const int ii = I0 + row, jj = J0 + row;
-        const bool kin = k < R;
-        UI[row * LD + k] = (kin && ii < n) ? xs[(size_t)ii * D + 2 + k] : 0.f;
-        VI[row * LD + k] = (kin && ii < n) ? xs[(size_t)ii * D + 2 + R + k] : 0.f;
-        UJ[row * LD + k] = (kin && jj < n) ? xs[(size_t)jj * D + 2 + k] : 0.f;
-        VJ[row * LD + k] = (kin && jj < n) ? xs[(size_t)jj * D + 2 + R + k] : 0.f;
-    }
-    if (threadIdx.x < AME_TILE) {
-        const int row = threadIdx.x;
-        const int ii = I0 + row, jj = J0 + row;
-        aI[row] = ii < n ? xs[(size_t)ii * D + 0] : 0.f;
-        bI[row] = ii < n ? xs[(size_t)ii * D + 1] : 0.f;
-        aJ[row] = jj < n ? xs[(size_t)jj * D + 0] : 0.f;
-        bJ[row] = jj < n ? xs[(size_t)jj * D + 1] : 0.f;
-    }
-    __syncthreads();
-
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int qi = w >> 1, qj = w & 1;
-    const int lr = lane & 15, lk = lane >> 4;
-    const float p = (float)r00, q01 = (float)r01, q10 = (float)r10, s = (float)r11;
     const float* ys = Yt + (size_t)tl * n * n * 2;
+    const float p = (float)r00, q01 = (float)r01, q10 = (float)r10, sr = (float)r11;
+
+    auto stage = [&](int J, int buf) {
+        const int J0 = J * AME_TILE;
+        for (int idx = threadIdx.x; idx < AME_TILE * RP; idx += AME_NT) {
+            const int row = idx / RP, k = idx - row * RP;
+            const int jj = J0 + row;
+            const bool ok = k < R && jj < n;
+            UJ[buf][row * LD + k] = ok ? xs[(size_t)jj * D + 2 + k] : 0.f;
+            VJ[buf][row * LD + k] = ok ? xs[(size_t)jj * D + 2 + R + k] : 0.f;
+        }
+        if (threadIdx.x < AME_TILE) {
+            const int jj = J0 + threadIdx.x;
+            aJ[buf][threadIdx.x] = jj < n ? xs[(size_t)jj * D + 0] : 0.f;
+            bJ[buf][threadIdx.x] = jj < n ? xs[(size_t)jj * D + 1] : 0.f;
+        }
+    };
+
     double quad = 0.0, sq = 0.0;
+    const int nstrip = (swap_mode && nb - 1 - s != s) ? 2 : 1;
+    for (int st = 0; st < nstrip; ++st) {
+        const int I = (st == 0) ? s : nb - 1 - s;
+        const int I0 = I * AME_TILE;
+        const int i = I0 + 16 * w + li;          // this lane's row (C column)
+        const bool irow = i < n;
+        // B operands: U_I / V_I [row i][k0 + lq]; lane's own a_i, b_i
+        float bu[RP / 4], bv[RP / 4];
 #pragma unroll
-    for (int si = 0; si < 2; ++si) {
+        for (int kk = 0; kk < RP / 4; ++kk) {
+            const int k = 4 * kk + lq;
+            bu[kk] = (irow && k < R) ? xs[(size_t)i * D + 2 + k] : 0.f;
+            bv[kk] = (irow && k < R) ? xs[(size_t)i * D + 2 + R + k] : 0.f;
+        }
+        const float ai = irow ? xs[(size_t)i * D + 0] : 0.f;
+        const float bi = irow ? xs[(size_t)i * D + 1] : 0.f;
+        const int Jb = swap_mode ? I : 0;
+        __syncthreads();   // the previous strip's last tile is done with both buffers
+        stage(Jb, 0);
+        __syncthreads();
+        for (int J = Jb; J < nb; ++J) {
+            const int buf = (J - Jb) & 1;
+            if (J + 1 < nb) stage(J + 1, buf ^ 1);
+            const int J0 = J * AME_TILE;
+            // Y runs of the 4 sub-tiles: row i, columns J0 + 16 sub + 4 lq .. +3
+            float4 y[4][2];
 #pragma unroll
-        for (int sj = 0; sj < 2; ++sj) {
-            const int ii0 = qi * 32 + si * 16, jj0 = qj * 32 + sj * 16;
-            f32x4 g1 = {0.f, 0.f, 0.f, 0.f}, g2 = {0.f, 0.f, 0.f, 0.f};
+            for (int sub = 0; sub < 4; ++sub) {
+                const int j0 = J0 + 16 * sub + 4 * lq;
+                if (irow && j0 + 4 <= n && (n & 1) == 0) {   // 16-byte aligned run inside the row
+                    const float4* yp = (const float4*)(ys + ((size_t)i * n + j0) * 2);
+                    y[sub][0] = yp[0];
+                    y[sub][1] = yp[1];
+                } else {                                      // row end / odd n: per element
+                    float t[8];
 #pragma unroll
-            for (int k0 = 0; k0 < RP; k0 += 4) {
-                const float a1 = UI[(ii0 + lr) * LD + k0 + lk];
-                const float b1 = VJ[(jj0 + lr) * LD + k0 + lk];
-                g1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, g1, 0, 0, 0);
-                const float a2 = VI[(ii0 + lr) * LD + k0 + lk];
-                const float b2 = UJ[(jj0 + lr) * LD + k0 + lk];
-                g2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a2, b2, g2, 0, 0, 0);
-            }
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                const int ii = ii0 + lk * 4 + v, jj = jj0 + lr;
-                const int i = I0 + ii, j = J0 + jj;
-                if (i >= n || j >= n || i == j) continue;
-                if (swap_mode && i > j) continue;
-                const float2 y = *(const float2*)(ys + ((size_t)i * n + j) * 2);
-                const float mu0 = (aI[ii] + bJ[jj]) + g1[v];
-                const float mu1 = (aJ[jj] + bI[ii]) + g2[v];
-                const float e0 = y.x - mu0, e1 = y.y - mu1;
-                const float se = e0 * e0 + e1 * e1;
-                if (i < j) {
-                    quad += (double)(e0 * (p * e0 + q01 * e1) + e1 * (q10 * e0 + s * e1));
-                    sq += swap_mode ? 2.0 * (double)se : (double)se;
-                } else {
-                    sq += (double)se;
+                    for (int e = 0; e < 4; ++e) {
+                        const bool ok = irow && j0 + e < n;
+                        const float2 v = ok ? *(const float2*)(ys + ((size_t)i * n + j0 + e) * 2)
+                                            : make_float2(0.f, 0.f);
+                        t[2 * e] = v.x;
+                        t[2 * e + 1] = v.y;
+                    }
+                    y[sub][0] = make_float4(t[0], t[1], t[2], t[3]);
+                    y[sub][1] = make_float4(t[4], t[5], t[6], t[7]);
                 }
             }
+#pragma unroll
+            for (int sub = 0; sub < 4; ++sub) {
+                f32x4 g1 = {0.f, 0.f, 0.f, 0.f}, g2 = {0.f, 0.f, 0.f, 0.f};
+                const int jr = 16 * sub + li;     // A operand row (column j of the tile)
+#pragma unroll
+                for (int kk = 0; kk < RP / 4; ++kk) {
+                    const float av = VJ[buf][jr * LD + 4 * kk + lq];
+                    const float au = UJ[buf][jr * LD + 4 * kk + lq];
+                    g1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bu[kk], g1, 0, 0, 0);
+                    g2 = __builtin_amdgcn_mfma_f32_16x16x4f32(au, bv[kk], g2, 0, 0, 0);
+                }
+                const float yv[8] = {y[sub][0].x, y[sub][0].y, y[sub][0].z, y[sub][0].w,
+                                     y[sub][1].x, y[sub][1].y, y[sub][1].z, y[sub][1].w};
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const int jl = 16 * sub + 4 * lq + v;
+                    const int j = J0 + jl;
+                    if (!irow || j >= n || i == j) continue;
+                    if (swap_mode && i > j) continue;
+                    const float mu0 = (ai + bJ[buf][jl]) + g1[v];
+                    const float mu1 = (aJ[buf][jl] + bi) + g2[v];
+                    const float e0 = yv[2 * v] - mu0, e1 = yv[2 * v + 1] - mu1;
+                    const float se = e0 * e0 + e1 * e1;
+                    if (i < j) {
+                        quad += (double)(e0 * (p * e0 + q01 * e1) + e1 * (q10 * e0 + sr * e1));
+                        sq += swap_mode ? 2.0 * (double)se : (double)se;
+                    } else {
+                        sq += (double)se;
+                    }
+                }
+            }
+            __syncthreads();
         }
     }
     double v2[2] = {quad, sq};
@@ -246,7 +291,7 @@ ame_final_kernel(const double* __restrict__ p2, int n2, const double* __restrict
 
 static inline long long pairs_blocks(const ame_dims* dm, int swap_mode) {
     const long long nb = (dm->n + AME_TILE - 1) / AME_TILE;
-    return (long long)dm->T_local * (swap_mode ? nb * (nb + 1) / 2 : nb * nb);
+    return (long long)dm->T_local * (swap_mode ? (nb + 1) / 2 : nb);
 }
 static inline long long nodes_blocks(const ame_dims* dm) {
     return ((long long)dm->T_local * dm->n + AME_NT - 1) / AME_NT;

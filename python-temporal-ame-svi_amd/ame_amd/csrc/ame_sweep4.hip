@@ -1,46 +1,36 @@
-// K1 (v3): latency-optimised Gauss-Seidel sweep of TemporalAMEStructuredMFVI /
-// TemporalAMENaiveMFVI on gfx950 -- new means AND new covariances of every
-// (node, time) step.
+// K1 (v4): Gauss-Seidel sweep of TemporalAMEStructuredMFVI / TemporalAMENaiveMFVI
+// on gfx950 with the observation natural parameter formed by MFMA block GEMMs.
 //
 // Reference semantics (Alfieriek/Python-Temporal-AME-SVI):
 //   _update_step                structured_mf.py:211-218  (for i in range(n))
 //   _update_node_i              structured_mf.py:220-287  (for t in range(T))
 //   _compute_observation_terms  structured_mf.py:289-326
 //   naive variant               naive_mf.py:207-282
-// Step (i,t) reads the NEW means of nodes j<i at t and of node i at t-1 and the
-// OLD means of nodes j>i at t and of node i at t+1 (2-D wavefront).
 //
-// Design (the algebra is restated and checked on CPU in
-// tests/test_sweep_algebra.py):
-//  * one 512-thread workgroup per time slice ("lane" t), all co-resident;
-//    lane t-1 hands mu_{i,t-1}^new to lane t through {epoch,value} granules;
-//  * wave 0 = SOLVER.  The only work between node i-1's new mean and node i's
-//    is one d x 2r matvec with the fp64 base inverse B_i (rows in registers),
-//    one 20-value cross-lane reduction and 2x2 algebra:
-//       K_i  = B_i - L_{i-1} W_{i-1}^T + G_{i-1} X_{i-1}^T   (applied lazily)
-//       W_i  = K_i J_{i-1}^T ,  M_i = R + J_{i-1} W_i ,  L_i = W_i M_i^-1
-//       mu_i = u_i + W_i M_i^-1 (y_{i,i-1} - J_{i-1} u_i) ,  u_i = K_i g_i
-//       X_i  = P_i^-1 J_{i+1}^T , S_i = R - J_{i+1} X_i , G_i = X_i S_i^-1
-//  * waves 1-7 = HELPERS (448 lanes), one step behind / ahead of the solver:
-//       HB  next base K_i = B_i + rank-4, fused with node i-1's covariance
-//           P_{i-1}^-1 = B_i - L_{i-1} W_{i-1}^T, damped and stored (hw 0-5);
-//       HE  h_obs GEMV of node i+2 over the slice's (U,V): register-resident
-//           (node j -> helper lane j % 448, slot j / 448), overflow in LDS;
-//       HF1 AR(1) terms + natural parameter g_{i+1} (hw 0-2);
-//       HF2 v_{i+1} = K_i g_{i+1}, yv_{i+1} = K_i J_{i+2}^T (hw 3-6);
-//       HX  the 20 dot products of the step that do not involve mu_{i-1} (hw 3);
-//       LOADER (hw 6): LDS-DMA (global_load_lds) rings, 3 steps ahead, for Y
-//           rows, old covariances, old means and the hand-off granules, so no
-//           wave holds prefetch registers.
-//  * one workgroup barrier per step; intra-step hand-offs through LDS
-//    counters;
-//  * the slice's base inverse P_0^-1 is formed in the prologue (fp64 sums over
-//    the slice's old means + symmetric sweep operator), so a slice can start
-//    as soon as its own inputs exist: with wait_epoch set, the workgroup of
-//    slice t first waits until the previous sweep has finished slices t and
-//    t+1 (per-slice done flags, agent-scope release / acquire).  The next sweep
-//    is then queued while this one runs, and consecutive sweeps overlap instead
-//    of each paying the wavefront fill.
+// Same solver / helper-wave structure and Woodbury algebra as v3
+// (ame_sweep3.hip, restated in tests/test_sweep_algebra.py).  What changes is
+// h_obs(m) = sum_{j != m} J_j^T z_mj (z = R^-1 y; new means for j < m, old for
+// j > m).  v3 formed it per step as a 1024-long GEMV on seven helper waves,
+// each ending in a 34-value cross-lane reduce-scatter: ~60 % of the step's VALU
+// work.  v4 splits it (schedule checked on the CPU by
+// tests/test_sweep4_schedule.py):
+//   * block GEMM: for the 16 nodes of block b, every column j outside the
+//     window W(b) = [16b - 22, 16b + 16), on v_mfma_f32_16x16x4_f32
+//     (A = z of the block's Y rows, B = the slice's (U, V) from a transposed
+//     HBM copy Mt), spread over the 16 helper steps [16b - 18, 16b - 2) on
+//     four helper waves (4 K-steps each per step), partials reduced in fp64;
+//   * window GEMV: at step m - 2, the <= 34 columns of W(b) other than
+//     m-3 .. m, from a 64-slot LDS ring of (U, V) rows (old rows DMA'd 22
+//     steps ahead, new rows written as nodes finish), two half-waves;
+//   * HF1 (step m - 1) adds nodes m - 3 and m - 2; the solver adds m - 1.
+// Columns outside the window read new means only for j < 16b - 22, which
+// every copy has by the time the GEMM loads them (Mt store of node j at step
+// j + 1, drained at the start of step j + 2, loaded from step j + 3), and old means for
+// j >= 16b + 16, which nothing has touched yet.
+//
+// Accuracy: each GEMM output is 4 fp32 MFMA chains of <= n/64 K-steps per
+// wave, summed in fp32 pairs then in fp64 over the 4 waves; the window is
+// <= 16 sequential fp32 terms per half; HF1 adds everything in fp64.
 #include "ame_common.h"
 #include "ame_wave.h"
 #include "ame_sweep_dev.h"
@@ -48,59 +38,56 @@
 using namespace ame;
 
 #ifdef AME_STAMPS
-// Diagnostic build only (cdna_hip_programming.md §7, in-kernel stamps): the
-// middle lane records s_memtime at marked points of steps [S3_I0, S3_I0+16) for
-// waves 0 (solver), 1 (hw 0), 4 (hw 3) and 7 (hw 6); every lane records
-// s_memrealtime when it reaches steps 0, n/4, n/2, 3n/4 and n.
-#define S3_I0 256
-__device__ unsigned long long g_s3_stamps[4 * 16 * 16];
-__device__ unsigned long long g_s3_prog[256 * 5];
-__device__ unsigned int g_s3_hwid[8];
-#define S3W(w) ((w) == 0 ? 0 : (w) == 1 ? 1 : (w) == 6 ? 2 : (w) == 7 ? 3 : -1)
-#define STAMP3(slot)                                                                           \
+#define S4_I0 256
+__device__ unsigned long long g_s4_stamps[5 * 16 * 16];
+__device__ unsigned long long g_s4_prog[256 * 5];
+#define S4W(w) ((w) == 0 ? 0 : (w) == 1 ? 1 : (w) == 4 ? 2 : (w) == 5 ? 3 : (w) == 7 ? 4 : -1)
+#define STAMP4(slot)                                                                           \
     do {                                                                                       \
-        if (tl == TL / 2 && lane == 0 && i >= S3_I0 && i < S3_I0 + 16 && S3W(wave) >= 0) {     \
+        if (tl == TL / 2 && lane == 0 && i >= S4_I0 && i < S4_I0 + 16 && S4W(wave) >= 0) {     \
             unsigned long long t_;                                                             \
             __builtin_amdgcn_sched_barrier(0);                                                 \
             asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");        \
             __builtin_amdgcn_sched_barrier(0);                                                 \
-            g_s3_stamps[(S3W(wave) * 16 + (i - S3_I0)) * 16 + (slot)] = t_;                    \
+            g_s4_stamps[(S4W(wave) * 16 + (i - S4_I0)) * 16 + (slot)] = t_;                    \
         }                                                                                      \
     } while (0)
-#define PROG3()                                                                                \
+#define PROG4()                                                                                \
     do {                                                                                       \
         if (tid == 0 && (i == 0 || i == n / 4 || i == n / 2 || i == 3 * n / 4 || i == n)) {    \
             const int q_ = (i == 0) ? 0 : (i == n / 4) ? 1 : (i == n / 2) ? 2 : (i == 3 * n / 4) ? 3 : 4; \
-            g_s3_prog[tl * 5 + q_] = __builtin_amdgcn_s_memrealtime();                         \
+            g_s4_prog[tl * 5 + q_] = __builtin_amdgcn_s_memrealtime();                         \
         }                                                                                      \
     } while (0)
-extern "C" int ame_debug_read_hwid3(unsigned int* h) {
-    return hipMemcpyFromSymbol(h, HIP_SYMBOL(g_s3_hwid), sizeof(g_s3_hwid), 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
-}
-extern "C" int ame_debug_read_stamps3(unsigned long long* st, unsigned long long* prog) {
-    if (hipMemcpyFromSymbol(st, HIP_SYMBOL(g_s3_stamps), sizeof(g_s3_stamps), 0, hipMemcpyDeviceToHost) != hipSuccess)
+extern "C" int ame_debug_read_stamps4(unsigned long long* st, unsigned long long* prog) {
+    if (hipMemcpyFromSymbol(st, HIP_SYMBOL(g_s4_stamps), sizeof(g_s4_stamps), 0, hipMemcpyDeviceToHost) != hipSuccess)
         return -1;
-    return hipMemcpyFromSymbol(prog, HIP_SYMBOL(g_s3_prog), sizeof(g_s3_prog), 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+    return hipMemcpyFromSymbol(prog, HIP_SYMBOL(g_s4_prog), sizeof(g_s4_prog), 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #else
-#define STAMP3(slot) do { } while (0)
-#define PROG3() do { } while (0)
+#define STAMP4(slot) do { } while (0)
+#define PROG4() do { } while (0)
 #endif
 
 namespace {
 
-constexpr int kNT = 512;    // threads per workgroup
-constexpr int kNH = 448;    // helper lanes
-constexpr int kMREG = 96;   // VGPR budget for the register-resident part of the node slice
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kNT = 512;     // threads per workgroup: solver wave + 7 helper waves
+constexpr int kBS = 16;      // GEMM block: 16 nodes (MFMA rows)
+constexpr int kGL = 22;      // window lead: W(b) = [16b - kGL, 16b + kBS)
+constexpr int kGS = 18;      // GEMM of block b runs at helper steps [16b - kGS, 16b - 2)
+constexpr int kVM = 2;       // 16-column groups per GEMM wave per step (n <= 2048)
+constexpr int kMR = 64;      // (U, V) ring slots
+constexpr int kYW = 8;       // Y window ring slots (1 KiB = 128 columns each)
+constexpr int kLAG = 6;      // slice t starts once slice t-1 has finished this node (see prologue)
 constexpr int kLDSMAX = 160 * 1024;
 
+__host__ __device__ constexpr int al16(int x) { return (x + 15) & ~15; }
+
 template <int R>
-struct Cfg {
+struct Cfg4 {
     static constexpr int D = 2 + 2 * R, M2 = 2 * R, DD = D * D;
-    // node j -> helper lane j % 448, slot j / 448; slots < NSREG in registers,
-    // further slots in LDS ([slot][c/2][lane] float2: conflict-free reads)
-    static constexpr int NSREG = (kMREG / M2) < 1 ? 1 : ((kMREG / M2) > 16 ? 16 : (kMREG / M2));
-    static constexpr int MP = (M2 + 1) / 2;
     static constexpr int NLT = D * (D + 1) / 2;
     static constexpr int NHB = 384;                           // HB lanes (hw 0-5)
     static constexpr int LTQ = (NLT + NHB - 1) / NHB;
@@ -111,74 +98,79 @@ struct Cfg {
     static constexpr int NC = (DD * 4 + 1023) / 1024;       // DMA KiB per covariance
 };
 
-// LDS carve-up (bytes); host and device agree.  Everything but the Y ring and
-// the overflow node slots has a compile-time offset (folds into ds_* immediate
-// offsets instead of occupying SGPRs).  Ring slots are whole KiB multiples: one
-// LDS-DMA instruction writes 64 lanes x 16 B = 1 KiB.
-__host__ __device__ constexpr int al16(int x) { return (x + 15) & ~15; }
+// LDS carve-up (bytes), all compile-time: nothing scales with n.
 template <int R>
-struct Lay {
+struct Lay4 {
     static constexpr int D = 2 + 2 * R, DD = D * D;
     static constexpr int cs = ((DD * 4 + 1023) / 1024) * 256;     // covariance ring slot (floats)
     static constexpr int oK = 0;                                   // base inverse, double buffer
     static constexpr int NPA = (4 * D <= 192) ? 4 : 2;
-    static constexpr int MCP = ((D + NPA - 1) / NPA) * NPA;       // AR row stride (zero padded)
-    static constexpr int oAR = al16(oK + 8 * 2 * DD);              // Qinv Phi, Phi^T Qinv (fp64) [D][MCP]
+    static constexpr int MCP = ((D + NPA - 1) / NPA) * NPA;
+    static constexpr int oAR = al16(oK + 8 * 2 * DD);              // Qinv Phi, Phi^T Qinv [D][MCP]
     static constexpr int oRec = al16(oAR + 8 * 2 * D * MCP);       // [par][k]{L0 L1 W0 W1 G0 G1 X0 X1}
-    static constexpr int oMu64 = al16(oRec + 8 * 2 * D * 8);       // [par][k] new mean (fp64)
-    static constexpr int oMu32 = al16(oMu64 + 8 * 2 * D);          // [par][k] new mean (fp32)
-    static constexpr int oG = al16(oMu32 + 4 * 2 * D);             // [node&1][k] g of node
-    static constexpr int oJn = al16(oG + 8 * 2 * D);               // [q][k] J rows of node i+2 (old)
-    static constexpr int oV = al16(oJn + 8 * 2 * D);               // [node&1][k]{v, yv0, yv1, vA}
-    static constexpr int oDots = al16(oV + 8 * 2 * D * 4);         // HX results
-    static constexpr int oRed = al16(oDots + 8 * 32);              // solver reduction gather
-    static constexpr int oGP = al16(oRed + 8 * 64);                // [node&1][wave][k] GEMV partials
-    static constexpr int oYst = al16(oGP + 4 * 2 * 7 * D);         // [node&3]{y(m,m-1), y(m,m-2)} raw
-    static constexpr int oMuL = al16(oYst + 4 * 4 * 4);            // [wave][64] mu_{m,t-1}, zero padded
-    static constexpr int oPd = al16(oMuL + 4 * 3 * 64);            // [par][k] naive diag(P)
-    static constexpr int oPc = al16(oPd + 8 * 2 * D);              // [k] diag of Pconst(t) (naive)
-    static constexpr int oFlag = al16(oPc + 8 * D);                // kcnt, ddone, gcnt
+    static constexpr int oMu64 = al16(oRec + 8 * 2 * D * 8);
+    static constexpr int oMu32 = al16(oMu64 + 8 * 2 * D);
+    static constexpr int oG = al16(oMu32 + 4 * 2 * D);
+    static constexpr int oJn = al16(oG + 8 * 2 * D);
+    static constexpr int oV = al16(oJn + 8 * 2 * D);
+    static constexpr int oDots = al16(oV + 8 * 2 * D * 4);
+    static constexpr int oRed = al16(oDots + 8 * 32);
+    static constexpr int oWP = al16(oRed + 8 * 64);                // [m&1][half][k] window partials (f32)
+    static constexpr int oHB = al16(oWP + 4 * 2 * 2 * D);          // [b&1][row][k] block h (f64)
+    static constexpr int oGP = al16(oHB + 8 * 2 * kBS * D);        // [wave][row][k] GEMM partials (f32)
+    static constexpr int oGS = al16(oGP + 4 * 4 * kBS * D);        // [wave][kq][row][2] z row sums (f32)
+    static constexpr int oMuL = al16(oGS + 4 * 4 * 4 * kBS * 2);   // [wave][64] mu_{m,t-1}
+    static constexpr int oPd = al16(oMuL + 4 * 3 * 64);
+    static constexpr int oPc = al16(oPd + 8 * 2 * D);
+    static constexpr int oFlag = al16(oPc + 8 * D);
     static constexpr int oCr = al16(oFlag + 16);                   // [node&3] old covariances, DMA
     static constexpr int oXr = al16(oCr + 4 * 4 * cs);             // [node&7] old means slice t, DMA
     static constexpr int oRr = al16(oXr + 8 * 256);                // [node&3] old means slice t+1, DMA
     static constexpr int oPr = al16(oRr + 4 * 256);                // [node&3] hand-off granules, DMA
-    static constexpr int oYr = al16(oPr + 4 * 1024);               // [node&3] Y rows (raw), DMA
-    __host__ __device__ static int ys(int n) { return ((n * 8 + 1023) / 1024) * 128; }   // float2
-    __host__ __device__ static int oML(int n) { return al16(oYr + 4 * 8 * ys(n)); }
-    __host__ __device__ static int total(int n, int nsreg) {
-        const int nsl = (n + 447) / 448 - nsreg;
-        return al16(oML(n) + 8 * (nsl > 0 ? nsl : 0) * ((2 * R + 1) / 2) * 448);
-    }
+    static constexpr int oYw = al16(oPr + 4 * 1024);               // [row&7] Y window rows, DMA
+    static constexpr int oMR = al16(oYw + kYW * 1024);             // [node&63][64] (U,V) ring
+    static constexpr int total = al16(oMR + kMR * 256);
 };
+
+// J entries for state index k from a ring row [U(R), V(R)]:
+// J0 = [1, 0, V, 0], J1 = [0, 1, 0, U].
+template <int R>
+__device__ __forceinline__ void jcol_uv(const float* uv, int k, double& j0, double& j1) {
+    constexpr int D = 2 + 2 * R;
+    const bool ku = (k >= 2 && k < 2 + R), kv = (k >= 2 + R && k < D);
+    const double v = (double)uv[ku ? (k + R - 2) : (kv ? (k - 2 - R) : 0)];
+    j0 = (k == 0) ? 1.0 : (ku ? v : 0.0);
+    j1 = (k == 1) ? 1.0 : (kv ? v : 0.0);
+}
+
+__device__ __forceinline__ int win_lo(int b) { return max(0, kBS * b - kGL); }
 
 }  // namespace
 
 template <int R>
 __global__ void __launch_bounds__(kNT)
-ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
-    using C = Cfg<R>;
-    constexpr int D = C::D, M2 = C::M2, DD = C::DD, NSREG = C::NSREG, MP = C::MP;
+ame_sweep4_kernel(ame_dims dm, ame_sweep_args a) {
+    using C = Cfg4<R>;
+    constexpr int D = C::D, M2 = C::M2, DD = C::DD;
     constexpr int NLT = C::NLT, LTQ = C::LTQ, NP = C::NP, MC = C::MC, NHALF = C::NHALF, HD = C::HD;
     constexpr int NC = C::NC;
     const int n = dm.n, TL = dm.T_local, Tt = dm.T_total;
+    const int ns = (n + 15) & ~15;            // Mt row stride (floats)
+    const int NG = ns >> 4;                   // 16-column groups
     const int b = blockIdx.x;
-    // XCD-aware lane order: consecutive time slices share an XCD (speed only)
-    const int tl = (TL % 8 == 0) ? ((b & 7) * (TL >> 3) + (b >> 3)) : b;
+    const int tl = (TL % 8 == 0) ? ((b & 7) * (TL >> 3) + (b >> 3)) : b;   // XCD-aware (speed only)
     const int tg = dm.t_begin + tl;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int hl = tid - 64, hw = wave - 1;   // helper lane / helper wave (valid for wave >= 1)
+    const int hl = tid - 64, hw = wave - 1;
     const bool is_naive = dm.variant == AME_NAIVE, is_bad = dm.variant == AME_BAD;
-    const int ns = (n + kNH - 1) / kNH;
-    const int NY = (n * 8 + 1023) / 1024;     // DMA KiB per Y row
-    const int KDMA = NY + NC + 3;             // DMA instructions per step (loader wave)
+    constexpr int KDMA = NC + 5;              // DMA instructions per step (loader wave)
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    using LY = Lay<R>;
-    const int YS = LY::ys(n);
+    using LY = Lay4<R>;
     double* Kbuf = (double*)(smem + LY::oK);
     constexpr int MCP = LY::MCP;
-    double* arQ = (double*)(smem + LY::oAR);          // Qinv Phi   [D][MCP]
-    double* arP = arQ + D * MCP;                       // Phi^T Qinv [D][MCP]
+    double* arQ = (double*)(smem + LY::oAR);
+    double* arP = arQ + D * MCP;
     double* rec = (double*)(smem + LY::oRec);
     double* mu64 = (double*)(smem + LY::oMu64);
     float* mu32 = (float*)(smem + LY::oMu32);
@@ -187,8 +179,10 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     double* vbuf = (double*)(smem + LY::oV);
     double* dots = (double*)(smem + LY::oDots);
     double* red = (double*)(smem + LY::oRed);
-    float* gp = (float*)(smem + LY::oGP);
-    float* yst = (float*)(smem + LY::oYst);
+    float* wpart = (float*)(smem + LY::oWP);
+    double* hblk = (double*)(smem + LY::oHB);
+    float* gpart = (float*)(smem + LY::oGP);
+    float* gsum = (float*)(smem + LY::oGS);
     float* muL = (float*)(smem + LY::oMuL);
     double* pdl = (double*)(smem + LY::oPd);
     double* pcdl = (double*)(smem + LY::oPc);
@@ -196,25 +190,23 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     uint32_t* kcnt = flags;
     uint32_t* ddone = flags + 1;
     uint32_t* gcnt = flags + 2;
-    float2* yring = (float2*)(smem + LY::oYr);
     float* cring = (float*)(smem + LY::oCr);
     float* xring = (float*)(smem + LY::oXr);
     float* rring = (float*)(smem + LY::oRr);
     uint64_t* pring = (uint64_t*)(smem + LY::oPr);
-    float2* mlds = (float2*)(smem + LY::oML(n));
+    float2* ywin = (float2*)(smem + LY::oYw);
+    float* mring = (float*)(smem + LY::oMR);
 
     const double r00 = a.rinv[0], r01 = a.rinv[1], r10 = a.rinv[2], r11 = a.rinv[3];
     const float r00f = (float)r00, r01f = (float)r01, r10f = (float)r10, r11f = (float)r11;
-    const Mat2 Rm = inv2s(m2(r00, r01, r10, r11));   // R = R_inv^-1, symmetrised
+    const Mat2 Rm = inv2s(m2(r00, r01, r10, r11));
     const float lr = a.lr, om = a.one_minus_lr;
     const float* xo = a.x_old + (size_t)tl * n * D;
     float* xn = a.x_new + (size_t)tl * n * D;
     float* cvs = a.cov + (size_t)tl * n * DD;
-    float* cvw = (a.cov_new != nullptr ? a.cov_new : a.cov) + (size_t)tl * n * DD;   // damped output
+    float* cvw = (a.cov_new != nullptr ? a.cov_new : a.cov) + (size_t)tl * n * DD;
     const float* ysl = a.Yt + (size_t)tl * n * n * 2;
-    // old means of slice t+1: the next local slice, or for the last local slice the
-    // right rank's first slice -- next_old (gathered before the sweep), or in a
-    // pipelined launch the back channel that rank fills when its slice finishes
+    float* Mt = (float*)a.work + (size_t)tl * M2 * ns;      // [2r][ns] current (U, V), transposed
     const bool back_rd = (a.wait_epoch != 0u) && (tl == TL - 1) && (a.back_in != nullptr);
     const float* xr = (tg < Tt - 1) ? ((tl < TL - 1) ? a.x_old + (size_t)(tl + 1) * n * D
                                                      : (back_rd ? a.back_in : a.next_old))
@@ -222,11 +214,10 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     const double* QiPhi = a.consts + 3 * (size_t)DD;
     bool dead = false;
 
-    // ---- hand-off of mu_{node, t-1} ----
+    // ---- hand-off of mu_{node, t-1} (as v3) ----
     auto gran_src = [&](int node) -> const uint64_t* {
         return (tl == 0) ? a.halo_in + (size_t)node * D : a.hand + ((size_t)(tl - 1) * n + node) * D;
     };
-    // v = granule of this lane (k = lane < D) as read earlier; spin until its tag is current
     auto gran_finish = [&](int node, uint64_t v, float* dst) {
         if (tg == 0) {
             if (lane < D) dst[lane] = 0.f;
@@ -255,18 +246,16 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         if (lane < D) dst[lane] = __uint_as_float((uint32_t)v);
     };
 
-    // ---- loader DMA pieces (whole-wave; every call issues a fixed instruction count) ----
-    auto dma_y = [&](int row) {   // Y row (raw float2) -> slot row & 3 : NY instructions
+    // ---- loader DMA pieces (whole-wave; fixed instruction count per call) ----
+    auto dma_yw = [&](int row) {   // Y row `row`, columns [win_lo, +128) -> slot row & 7 : 1 instruction
         const int rw = (row < n) ? row : 0;
-        const char* base = (const char*)(ysl + (size_t)rw * n * 2);
-        const uint32_t dst = lds_off(yring + (size_t)(row & 3) * YS);
-        for (int q = 0; q < NY; ++q) {
-            int off = (q * 64 + lane) * 16;
-            if (off >= n * 8) off = 0;
-            dma16(base + off, dst + q * 1024);
-        }
+        const int c0 = win_lo(rw >> 4);
+        const char* base = (const char*)(ysl + ((size_t)rw * n + c0) * 2);
+        int off = lane * 16;
+        if (c0 * 8 + off >= n * 8) off = 0;
+        dma16(base + off, lds_off(ywin + (size_t)(row & (kYW - 1)) * 128));
     };
-    auto dma_cov = [&](int node) {   // old covariance -> slot node & 3 : NC instructions
+    auto dma_cov = [&](int node) {
         const int cn = (node >= 0 && node < n) ? node : 0;
         const char* base = (const char*)(cvs + (size_t)cn * DD);
         const uint32_t dst = lds_off(cring + (size_t)(node & 3) * LY::cs);
@@ -277,34 +266,28 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             dma16(base + off, dst + q * 1024);
         }
     };
-    auto dma_x = [&](int node) {   // old mean, slice t -> slot node & 7 : 1 instruction
+    auto dma_x = [&](int node) {
         const int xnn = (node < n) ? node : 0;
         dma4(xo + (size_t)xnn * D + (lane < D ? lane : 0), lds_off(xring + (node & 7) * 64));
     };
-    auto dma_r = [&](int node) {   // old mean, slice t+1 -> slot node & 3 : 1 instruction
+    auto dma_r = [&](int node) {
         const float* src = (xr != nullptr && node < n) ? xr + (size_t)node * D : xo;
         if (back_rd) dma4_sys(src + (lane < D ? lane : 0), lds_off(rring + (node & 3) * 64));
         else dma4(src + (lane < D ? lane : 0), lds_off(rring + (node & 3) * 64));
     };
-    auto dma_p = [&](int node) {   // granules of mu_{node, t-1} -> slot node & 3 : 1 instruction
+    auto dma_p = [&](int node) {
         const uint32_t dst = lds_off(pring + (size_t)(node & 3) * 128);
         const int g2 = (lane * 2 < D) ? lane * 2 : 0;
         if (tg == 0 || node >= n) dma16(xo, dst);
         else if (tl == 0) dma16_sys(gran_src(node) + g2, dst);
         else dma16_sc1(gran_src(node) + g2, dst);
     };
+    auto dma_m = [&](int node) {   // old (U, V) of `node` -> ring slot node & 63 : 1 instruction
+        const int mn = (node < n) ? node : 0;
+        dma4(xo + (size_t)mn * D + 2 + (lane < M2 ? lane : 0), lds_off(mring + (node & (kMR - 1)) * 64));
+    };
 
-#ifdef AME_STAMPS
-    if (tl == TL / 2 && lane == 0) {
-        unsigned int hwid;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
-        g_s3_hwid[wave] = hwid;
-    }
-#endif
     // ============================ prologue ============================
-    // pipelined launch: the previous sweep must have finished slices t and t+1
-    // (their means and covariances are this sweep's inputs; slice t+1 also reads
-    // this slice's hand-off granules, which this sweep overwrites)
     if (a.wait_epoch != 0u) {
         if (tid == 0) {
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -318,7 +301,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                     __builtin_amdgcn_s_sleep(8);
                 }
             }
-            if (back_rd) {   // the right rank's first slice of the previous sweep
+            if (back_rd) {
                 const uint32_t* bd = (const uint32_t*)(a.back_in + AME_BACK_DONE_OFFSET(n * D));
                 while (__hip_atomic_load(const_cast<uint32_t*>(bd), __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_SYSTEM) < a.wait_epoch) {
@@ -335,15 +318,14 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         }
         __syncthreads();
     }
-    // P_0 = Pconst + sum_{j>=1} F_j(old), F_j = J_j^T R^-1 J_j (fp64), and its
-    // inverse -> Kbuf[0] by the in-place symmetric sweep operator; naive variant:
-    // column sums of squares of (U, V) over all nodes -> red[]
+    // P_0 = Pconst + sum_{j>=1} F_j(old) (fp64) and its inverse -> Kbuf[0]; naive:
+    // column sums of squares of (U, V) over all nodes -> red[]   (as v3)
     {
         constexpr int EQ = (NLT + kNT - 1) / kNT;
-        float* st = (float*)yring;   // staging: CH nodes x 2r (the rings are not live yet)
+        float* st = mring;   // staging: CH nodes x 2r (the ring is not live yet)
         double* piv = vbuf;
         double* K = Kbuf;
-        const int CH = min(64, (8 * YS) / M2);
+        constexpr int CH = (kMR * 64) / M2 < 64 ? (kMR * 64) / M2 : 64;
         const double pp = r00, ss = r11, qq = 0.5 * (r01 + r10);
         double acc[EQ];
         int ek[EQ], em[EQ];
@@ -370,7 +352,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 const int k = ek[u], m = em[u];
                 if (k < 2) continue;
                 const int ck = k - 2;
-                const int kc = (ck < R) ? R + ck : ck - R;   // row U_ck pairs with V, row V with U
+                const int kc = (ck < R) ? R + ck : ck - R;
                 double a0 = 0.0;
                 if (m < 2) {
                     for (int jj = 0; jj < cnt; ++jj) a0 += (double)st[jj * M2 + kc];
@@ -388,7 +370,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                     sq = fma(v, v, sq);
                 }
         }
-        if (tid < M2) {   // node 0 joins the sums of squares
+        if (tid < M2) {
             const double v = (double)xo[2 + tid];
             red[tid] = fma(v, v, sq);
         }
@@ -413,7 +395,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             K[m * D + k] = v;
         }
         __syncthreads();
-        for (int pv = 0; pv < D; ++pv) {   // K -> -P_0^-1
+        for (int pv = 0; pv < D; ++pv) {
             if (tid < D) piv[tid] = K[pv * D + tid];
             __syncthreads();
             const double rinv = 1.0 / piv[pv];
@@ -433,7 +415,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         for (int e = tid; e < DD; e += kNT) K[e] = -K[e];
         __syncthreads();
     }
-    for (int e = tid; e < 2 * D * MCP; e += kNT) {   // QiPhi, PhiTQi (adjacent in consts), padded
+    for (int e = tid; e < 2 * D * MCP; e += kNT) {
         const int mat = e / (D * MCP), rc = e - mat * D * MCP, rr = rc / MCP, cc = rc - rr * MCP;
         arQ[e] = (cc < D) ? QiPhi[(size_t)mat * DD + rr * D + cc] : 0.0;
     }
@@ -444,126 +426,168 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         mu64[e] = 0.0;
         mu32[e] = 0.f;
     }
-    if (tid < 16) yst[tid] = 0.f;
     if (tid < 4) flags[tid] = 0u;
-    float mreg[NSREG][M2];      // (U, V) of nodes hl + 448 s, s < NSREG
-    if (wave >= 1) {
-#pragma unroll
-        for (int s = 0; s < NSREG; ++s) {
-            const int j = hl + kNH * s;
-            const bool ok = s < ns && j < n;
-#pragma unroll
-            for (int c = 0; c < M2; ++c) mreg[s][c] = ok ? xo[(size_t)j * D + 2 + c] : 0.f;
-        }
-        for (int s = NSREG; s < ns; ++s) {
-            const int j = hl + kNH * s;
-            const bool ok = j < n;
-            for (int c2 = 0; c2 < MP; ++c2) {
-                float2 v = make_float2(0.f, 0.f);
-                if (ok) {
-                    v.x = xo[(size_t)j * D + 2 + 2 * c2];
-                    if (2 * c2 + 1 < M2) v.y = xo[(size_t)j * D + 3 + 2 * c2];
-                }
-                mlds[((s - NSREG) * MP + c2) * kNH + hl] = v;
-            }
-        }
-        // Y rows 0 and 1 into ring slots 0 and 1 (plain loads)
-        for (int e = hl; e < 2 * n; e += kNH) {
-            const int rw = e / n, j = e - rw * n;
-            yring[(size_t)rw * YS + j] = (rw < n) ? *(const float2*)(ysl + ((size_t)rw * n + j) * 2)
-                                                    : make_float2(0.f, 0.f);
-        }
+    // transposed (U, V) copy of the slice's old means (padding columns zero)
+    for (int e = tid; e < M2 * ns; e += kNT) {
+        const int c = e / ns, j = e - c * ns;
+        Mt[e] = (j < n) ? xo[(size_t)j * D + 2 + c] : 0.f;
     }
-    double ssq_l = 0.0;   // solver, naive: running sum of squares of column `lane`
+    __syncthreads();   // the P_0 staging in the ring region is no longer read
+    // (U, V) ring rows of nodes 0..19; Y windows of rows 0..4
+    for (int e = tid; e < kGL * 64; e += kNT) {
+        const int j = e >> 6, c = e & 63;
+        mring[e] = (j < n && c < M2) ? xo[(size_t)j * D + 2 + c] : 0.f;
+    }
+    for (int e = tid; e < 5 * 128; e += kNT) {
+        const int row = e >> 7, c = e & 127;
+        const int c0 = win_lo(row >> 4);
+        ywin[e] = (row < n && c0 + c < n) ? *(const float2*)(ysl + ((size_t)row * n + c0 + c) * 2)
+                                           : make_float2(0.f, 0.f);
+    }
+    double ssq_l = 0.0;
     if (tid < D && is_naive && tid >= 2) ssq_l = red[tid - 2];
-    if (wave == 7) {   // rings read by steps 0..2 and the prologue
+    if (wave == 7) {
         for (int q = 0; q < 5; ++q) dma_x(q);
         for (int q = 0; q < 4; ++q) dma_r(q);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // Mt stores and the DMAs
     __syncthreads();
 
-    // GEMV of node m over nodes j (excluding j in {m-2, m-1, m}) from raw Y values
-    // ysrc[j]; stashes y_{m,m-1}, y_{m,m-2}; partials -> gp[m&1][hw][.]
-    auto gemv = [&](int m, const float2* ysrc) {
-        float acc[D];
+    // ---------------- block GEMM (helper waves hw 0..3) ----------------
+    f32x4 accV[4], accU[4];
+    float rs0 = 0.f, rs1 = 0.f;
+    f32x4 pa0[kVM], pa1[kVM], pv[kVM], pu[kVM];
+    const int gw = hw;              // GEMM wave index (valid for hw 0..3)
+    const int grow = lane & 15, gkq = lane >> 4;
+    auto gemm_load = [&](int bb, int q) {
+        if (bb < 0 || kBS * bb >= n) return;
+        int m = kBS * bb + grow;
+        if (m >= n) m = n - 1;
+        const int cu = (grow < R) ? grow : 0;
 #pragma unroll
-        for (int c = 0; c < D; ++c) acc[c] = 0.f;
-        float2 yv[NSREG];
-#pragma unroll
-        for (int s = 0; s < NSREG; ++s) {   // ring slots are >= n long: loads need no guard
-            const int j = hl + kNH * s;
-            const float2 y = ysrc[j];
-            yv[s] = (j < n) ? y : make_float2(0.f, 0.f);
-        }
-#pragma unroll
-        for (int s = 0; s < NSREG; ++s) {
-            if (s < ns) {
-                const int j = hl + kNH * s;
-                const bool ex = (j >= m - 2) && (j <= m);
-                const float z0 = ex ? 0.f : r00f * yv[s].x + r01f * yv[s].y;
-                const float z1 = ex ? 0.f : r10f * yv[s].x + r11f * yv[s].y;
-                acc[0] += z0;
-                acc[1] += z1;
-#ifndef AME_ABL_GEMV_NOFMA
-#pragma unroll
-                for (int c = 0; c < R; ++c) {
-                    acc[2 + c] = fmaf(z0, mreg[s][R + c], acc[2 + c]);       // h_U += z0 V
-                    acc[2 + R + c] = fmaf(z1, mreg[s][c], acc[2 + R + c]);   // h_V += z1 U
-                }
-#endif
+        for (int v = 0; v < kVM; ++v) {
+            const int u = 4 * q + gw + 64 * v;
+            if (u < NG) {
+                int j0 = 16 * u + 4 * gkq;
+                const int jy = (j0 < n) ? j0 : 0;   // n % 4 == 0: a chunk is all in or all out
+                const float4* ya = (const float4*)(ysl + ((size_t)m * n + jy) * 2);
+                const float4 y0 = ya[0], y1 = ya[1];
+                pa0[v] = f32x4{y0.x, y0.y, y0.z, y0.w};
+                pa1[v] = f32x4{y1.x, y1.y, y1.z, y1.w};
+                const float4 bv = *(const float4*)(Mt + (size_t)(R + cu) * ns + j0);
+                const float4 bu = *(const float4*)(Mt + (size_t)cu * ns + j0);
+                pv[v] = f32x4{bv.x, bv.y, bv.z, bv.w};
+                pu[v] = f32x4{bu.x, bu.y, bu.z, bu.w};
             }
-        }
-        for (int s = NSREG; s < ns; ++s) {
-            const int j = hl + kNH * s;
-            float2 y = ysrc[j];
-            if (j >= n) y = make_float2(0.f, 0.f);
-            const bool ex = (j >= m - 2) && (j <= m);
-            const float z0 = ex ? 0.f : r00f * y.x + r01f * y.y;
-            const float z1 = ex ? 0.f : r10f * y.x + r11f * y.y;
-            acc[0] += z0;
-            acc[1] += z1;
-            const float2* ml = mlds + (size_t)(s - NSREG) * MP * kNH + hl;
-#pragma unroll
-            for (int c2 = 0; c2 < MP; ++c2) {   // column c: U_c -> h_V (z1), V_c -> h_U (z0)
-                const float2 t = ml[c2 * kNH];
-                const int c = 2 * c2;
-                if (c < R) acc[2 + R + c] = fmaf(z1, t.x, acc[2 + R + c]);
-                else acc[2 + (c - R)] = fmaf(z0, t.x, acc[2 + (c - R)]);
-                if (c + 1 < M2) {
-                    if (c + 1 < R) acc[2 + R + c + 1] = fmaf(z1, t.y, acc[2 + R + c + 1]);
-                    else acc[2 + (c + 1 - R)] = fmaf(z0, t.y, acc[2 + (c + 1 - R)]);
-                }
-            }
-        }
-        int idx;
-#ifndef AME_ABL_GEMV_NORED
-        const float v = wave_reduce_scatter<D>(acc, lane, idx);
-#else
-        const float v = acc[lane % D]; idx = lane;
-#endif
-        if (idx < D) gp[((m & 1) * 7 + hw) * D + idx] = v;
-        // raw y_{m,m-1}, y_{m,m-2} for the solver / HF1 (owner lanes only)
-        const int jm1 = m - 1, jm2 = m - 2;
-        if (jm1 >= 0 && (jm1 % kNH) == hl) {
-            const float2 y = ysrc[jm1];
-            yst[(m & 3) * 4 + 0] = y.x;
-            yst[(m & 3) * 4 + 1] = y.y;
-        }
-        if (jm2 >= 0 && (jm2 % kNH) == hl) {
-            const float2 y = ysrc[jm2];
-            yst[(m & 3) * 4 + 2] = y.x;
-            yst[(m & 3) * 4 + 3] = y.y;
         }
     };
+    auto gemm_compute = [&](int bb, int q) {
+        if (bb < 0 || kBS * bb >= n) return;
+        if (q == 0) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                accV[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+                accU[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+            rs0 = rs1 = 0.f;
+        }
+        const int wlo = win_lo(bb), whi = min(n, kBS * bb + kBS);
+        const bool colok = grow < R;
+#pragma unroll
+        for (int v = 0; v < kVM; ++v) {
+            const int u = 4 * q + gw + 64 * v;
+            if (u < NG) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int j = 16 * u + 4 * gkq + e;
+                    const float yx = (e < 2) ? pa0[v][2 * e] : pa1[v][2 * e - 4];
+                    const float yy = (e < 2) ? pa0[v][2 * e + 1] : pa1[v][2 * e - 3];
+                    const bool ok = (j < n) && (j < wlo || j >= whi);
+                    const float z0 = ok ? r00f * yx + r01f * yy : 0.f;
+                    const float z1 = ok ? r10f * yx + r11f * yy : 0.f;
+                    rs0 += z0;
+                    rs1 += z1;
+                    const float bvv = colok ? pv[v][e] : 0.f;
+                    const float buu = colok ? pu[v][e] : 0.f;
+                    accV[e] = __builtin_amdgcn_mfma_f32_16x16x4f32(z0, bvv, accV[e], 0, 0, 0);
+                    accU[e] = __builtin_amdgcn_mfma_f32_16x16x4f32(z1, buu, accU[e], 0, 0, 0);
+                }
+            }
+        }
+        if (q == 15) {   // block done: this wave's partial -> LDS
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const int row = 4 * gkq + v, col = grow;
+                const float sV = (accV[0][v] + accV[1][v]) + (accV[2][v] + accV[3][v]);
+                const float sU = (accU[0][v] + accU[1][v]) + (accU[2][v] + accU[3][v]);
+                if (col < R) {
+                    gpart[(gw * kBS + row) * D + 2 + col] = sV;       // h_U = sum z0 V
+                    gpart[(gw * kBS + row) * D + 2 + R + col] = sU;   // h_V = sum z1 U
+                }
+            }
+            gsum[((gw * 4 + gkq) * kBS + grow) * 2 + 0] = rs0;
+            gsum[((gw * 4 + gkq) * kBS + grow) * 2 + 1] = rs1;
+        }
+    };
+    // block b's partials -> hblk[b & 1] (fp64, fixed order); one wave
+    auto gemm_reduce = [&](int bb) {
+        double* hb = hblk + (size_t)(bb & 1) * kBS * D;
+        for (int e = lane; e < kBS * D; e += 64) {
+            const int row = e / D, k = e - row * D;
+            double s = 0.0;
+            if (k < 2) {
+#pragma unroll
+                for (int w = 0; w < 4; ++w)
+#pragma unroll
+                    for (int kq = 0; kq < 4; ++kq) s += (double)gsum[((w * 4 + kq) * kBS + row) * 2 + k];
+            } else {
+#pragma unroll
+                for (int w = 0; w < 4; ++w) s += (double)gpart[(w * kBS + row) * D + k];
+            }
+            hb[e] = s;
+        }
+    };
+    // window GEMV of node m, half h: columns of W(m >> 4) with the same parity as
+    // win_lo + h, other than m-3 .. m  -> wpart[m & 1][h][.]
+    auto wgemv = [&](int m, int h) {
+        const int bb = m >> 4, c0 = win_lo(bb), c1 = min(n, kBS * bb + kBS);
+        const int k = lane;
+        const bool ku = (k >= 2 && k < 2 + R), kv = (k >= 2 + R && k < D);
+        const int src = ku ? (k + R - 2) : (kv ? (k - 2 - R) : 0);
+        const bool use_z1 = (k == 1) || kv;
+        const bool unit = k < 2;
+        const float2* yr = ywin + (size_t)(m & (kYW - 1)) * 128;
+        // fixed trip count (the window is at most kGL + kBS columns), predicated,
+        // so the compiler issues every LDS read of the half up front
+        constexpr int NWJ = (kGL + kBS + 1) / 2;
+        float yx[NWJ], yy[NWJ], mvv[NWJ];
+        bool okj[NWJ];
+#pragma unroll
+        for (int q = 0; q < NWJ; ++q) {
+            const int j = c0 + h + 2 * q;
+            okj[q] = j < c1 && (j < m - 3 || j > m);
+            const int jj = okj[q] ? j : c0;
+            const float2 y = yr[jj - c0];
+            yx[q] = y.x;
+            yy[q] = y.y;
+            mvv[q] = mring[(jj & (kMR - 1)) * 64 + src];
+        }
+        float acc = 0.f;
+#pragma unroll
+        for (int q = 0; q < NWJ; ++q) {
+            const float z0 = r00f * yx[q] + r01f * yy[q], z1 = r10f * yx[q] + r11f * yy[q];
+            const float f = okj[q] ? (unit ? 1.f : mvv[q]) : 0.f;
+            acc = fmaf(use_z1 ? z1 : z0, f, acc);
+        }
+        if (k < D) wpart[((m & 1) * 2 + h) * D + k] = acc;
+    };
     // HF1 (hw 0..2): AR terms + natural parameter g of node m.
-    // mu_{m,t-1} in muL[hw], mu_{m,t+1}^old in rring[m&3].
     auto hf1 = [&](int m) {
-        const int q = hl;   // 0..191
+        const int q = hl;
         const int k = q / NP, p = q - k * NP;
         const int kc = (k < D) ? k : 0;
-        const float* ml = muL + hw * 64;          // zero beyond D; zero when tg == 0
-        const float* mr = rring + (m & 3) * 64;   // finite beyond D (padded coefficients are 0)
+        const float* ml = muL + hw * 64;
+        const float* mr = rring + (m & 3) * 64;
         const double* aq = arQ + kc * MCP + p * MC;
         const double* ap = arP + kc * MCP + p * MC;
         double accL = 0.0, accR = 0.0;
@@ -576,22 +600,27 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         double acc = accL + ((tg < Tt - 1) ? accR : 0.0);
         acc = dpp_add_xor1(acc);
         if constexpr (NP == 4) acc = dpp_add_mirror4(acc);
-        // lane (k, 0) assembles g_k = GEMV partials + AR + node m-2's term
-        double g = 0.0;
-#pragma unroll
-        for (int w = 0; w < 7; ++w) g += (double)gp[((m & 1) * 7 + w) * D + kc];
+        const int bb = m >> 4, c0 = win_lo(bb);
+        double g = hblk[((bb & 1) * kBS + (m & 15)) * D + kc];
+        g += (double)wpart[((m & 1) * 2 + 0) * D + kc] + (double)wpart[((m & 1) * 2 + 1) * D + kc];
         g += acc;
-        if (m >= 2) {   // node m-2 was excluded from the GEMV; its new mean is known now
-            const float* mup = mu32 + ((m - 2) & 1) * D;
+        const float2* yr = ywin + (size_t)(m & (kYW - 1)) * 128;
+        if (m >= 3) {   // node m-3: new mean from the ring (written at step m-2)
             double j0, j1;
-            jcol<R>(mup, true, kc, j0, j1);
-            const double y0 = (double)yst[(m & 3) * 4 + 2], y1 = (double)yst[(m & 3) * 4 + 3];
-            const double z0 = r00 * y0 + r01 * y1, z1 = r10 * y0 + r11 * y1;
+            jcol_uv<R>(mring + ((m - 3) & (kMR - 1)) * 64, kc, j0, j1);
+            const float2 y = yr[m - 3 - c0];
+            const double z0 = r00 * (double)y.x + r01 * (double)y.y, z1 = r10 * (double)y.x + r11 * (double)y.y;
+            g = fma(j0, z0, fma(j1, z1, g));
+        }
+        if (m >= 2) {   // node m-2: the solver's LDS copy
+            double j0, j1;
+            jcol<R>(mu32 + ((m - 2) & 1) * D, true, kc, j0, j1);
+            const float2 y = yr[m - 2 - c0];
+            const double z0 = r00 * (double)y.x + r01 * (double)y.y, z1 = r10 * (double)y.x + r11 * (double)y.y;
             g = fma(j0, z0, fma(j1, z1, g));
         }
         if (k < D && p == 0) g64[(m & 1) * D + k] = g;
     };
-    // HF2 (hw 3..6): v = K g, yv = K Jn^T for node m with base Kb
     auto hf2 = [&](int m, const double* Kb) {
         const int q = tid - 256;
         const int k = q / (3 * NHALF), rem = q - k * (3 * NHALF);
@@ -611,7 +640,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             if (vsel == 0) vo[3] = accA;
         }
     };
-    auto jn_fill = [&](int node) {   // J rows of `node` (old) -> jn64; lanes < D of the calling wave
+    auto jn_fill = [&](int node) {
         if (lane < D) {
             double j0, j1;
             jcol<R>(xring + (node & 7) * 64, node < n, lane, j0, j1);
@@ -620,38 +649,46 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         }
     };
 
-    // ---- prologue work: g_0, GEMV partials of node 1, v_0 / yv_0; rings for steps 0..2 ----
-    if (wave >= 1) {
-        gemv(0, yring);
-        gemv(1, yring + YS);
-        if (hw <= 2) {
-            uint64_t g0 = 0;
-            if (tg > 0 && lane < D)
-                g0 = (tl == 0) ? gran_load_system(gran_src(0) + lane) : gran_load_agent(gran_src(0) + lane);
-            gran_finish(0, g0, muL + hw * 64);
-#ifdef AME_S3_LAG
-            // Experiment (off by default): keep slice t at least
-            // AME_S3_LAG + 1 node steps behind slice t-1, so the hand-off granules the
-            // loader DMAs 3 steps ahead of their use are already current and HF1
-            // skips the L2 poll.  Measured: step period unchanged (the loader and HX
-            // waves, not HF1, set it), plus a (AME_S3_LAG + 1)-step fill per slice.
-            if (hw == 0 && tg > 0 && n > 1) {
-                const int lagn = min(n - 1, AME_S3_LAG);
-                uint64_t gl = 0;
-                if (lane < D)
-                    gl = (tl == 0) ? gran_load_system(gran_src(lagn) + lane) : gran_load_agent(gran_src(lagn) + lane);
-                gran_finish(lagn, gl, (float*)red + 64);
+    // ---- prologue work: block h of blocks 0 and 1, window h of nodes 0 and 1,
+    // g_0, v_0 / yv_0; DMA rings for steps 0..2 ----
+    for (int bb = 0; bb < 2; ++bb) {
+        if (wave >= 1 && hw <= 3) {
+            for (int q = 0; q < 16; ++q) {
+                gemm_load(bb, q);
+                gemm_compute(bb, q);
             }
-#endif
         }
-        if (hw == 3) jn_fill(1);
+        __syncthreads();
+        if (wave == 7 && kBS * bb < n) gemm_reduce(bb);
+        __syncthreads();
     }
+    if (wave == 5 || wave == 6) {
+        wgemv(0, wave - 5);
+        if (n > 1) wgemv(1, wave - 5);
+    }
+    if (wave >= 1 && hw <= 2) {
+        uint64_t g0 = 0;
+        if (tg > 0 && lane < D)
+            g0 = (tl == 0) ? gran_load_system(gran_src(0) + lane) : gran_load_agent(gran_src(0) + lane);
+        gran_finish(0, g0, muL + hw * 64);
+        // Keep slice t at least kLAG + 1 steps behind slice t-1: then the hand-off
+        // granule the loader DMAs 3 steps ahead of its use is already current, and
+        // HF1 does not wait on the left slice's L2 round trip every step.  Costs a
+        // wavefront fill of (kLAG + 1) steps per slice once per pipelined fit().
+        if (hw == 0 && tg > 0 && n > 1) {
+            const int lagn = min(n - 1, kLAG);
+            uint64_t gl = 0;
+            if (lane < D)
+                gl = (tl == 0) ? gran_load_system(gran_src(lagn) + lane) : gran_load_agent(gran_src(lagn) + lane);
+            gran_finish(lagn, gl, (float*)red + 64);
+        }
+    }
+    if (wave == 4) jn_fill(1);
     __syncthreads();
     if (wave >= 1 && hw <= 2) hf1(0);
     __syncthreads();
     if (wave >= 4) hf2(0, Kbuf);
-    if (wave == 7) {   // Y rows 2..4 (slots 2,3,0), covariances of nodes 0,1, granules of nodes 1..3
-        for (int q = 2; q <= 4; ++q) dma_y(q);
+    if (wave == 7) {
         for (int q = 0; q <= 1; ++q) dma_cov(q);
         for (int q = 1; q <= 3; ++q) dma_p(q);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -659,32 +696,29 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     __syncthreads();
 
     if (wave == 0) {
-        // ============================ SOLVER ============================
-#ifndef AME_ABL_NOPRIO
+        // ============================ SOLVER (as v3) ============================
         __builtin_amdgcn_s_setprio(3);
-#endif
         const int k = lane;
         const bool kl = k < D;
         const int kc = kl ? k : 0;
-        double brow[D];   // row k of the base inverse B_i
+        double brow[D];
 #pragma unroll
         for (int c = 0; c < D; ++c) brow[c] = kl ? Kbuf[(size_t)k * D + c] : 0.0;
         double Wp0 = 0, Wp1 = 0, Xp0 = 0, Xp1 = 0, Lp0 = 0, Lp1 = 0, Gp0 = 0, Gp1 = 0;
         Mat2 Mip = m2(0, 0, 0, 0), Sip = m2(0, 0, 0, 0);
         for (int i = 0; i < n; ++i) {
-            PROG3();
-            STAMP3(0);
+            PROG4();
+            STAMP4(0);
             const int par = i & 1, ppar = (i + 1) & 1;
             const bool has_prev = i > 0;
-            const float* mup = mu32 + ppar * D;       // mu_{i-1} (fp32)
-            const double* mupd = mu64 + ppar * D;     // mu_{i-1} (fp64)
+            const float* mup = mu32 + ppar * D;
+            const double* mupd = mu64 + ppar * D;
             const double msk = kl ? 1.0 : 0.0;
             const double* vi = vbuf + (par * D + kc) * 4;
             const double v = msk * vi[0], yv0 = msk * vi[1], yv1 = msk * vi[2], vA = msk * vi[3];
             const double g = msk * g64[par * D + kc];
             double J0, J1;
             jcol<R>(mup, has_prev && kl, kc, J0, J1);
-            // kj = B J^T (the one critical matvec)
             double kj0 = 0, kj1 = 0;
             if (has_prev) {
                 double s0a = brow[0], s0b = 0, s1a = brow[1], s1b = 0;
@@ -700,16 +734,15 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 kj0 = s0a + s0b;
                 kj1 = s1a + s1b;
             }
-            STAMP3(1);
-            // critical reduction: a1(4) a2(4) c(4) e(2) jy(4) eA(2)
+            STAMP4(1);
             constexpr int NV = 20;
             double pr[NV];
-            pr[0] = Wp0 * J0; pr[1] = Wp0 * J1; pr[2] = Wp1 * J0; pr[3] = Wp1 * J1;       // a1[p][q]
-            pr[4] = Xp0 * J0; pr[5] = Xp0 * J1; pr[6] = Xp1 * J0; pr[7] = Xp1 * J1;       // a2[p][q]
-            pr[8] = J0 * kj0; pr[9] = J0 * kj1; pr[10] = J1 * kj0; pr[11] = J1 * kj1;     // c[q][p]
-            pr[12] = J0 * v; pr[13] = J1 * v;                                             // e[q]
-            pr[14] = J0 * yv0; pr[15] = J0 * yv1; pr[16] = J1 * yv0; pr[17] = J1 * yv1;   // jy[q][p]
-            pr[18] = J0 * vA; pr[19] = J1 * vA;                                           // eA[q]
+            pr[0] = Wp0 * J0; pr[1] = Wp0 * J1; pr[2] = Wp1 * J0; pr[3] = Wp1 * J1;
+            pr[4] = Xp0 * J0; pr[5] = Xp0 * J1; pr[6] = Xp1 * J0; pr[7] = Xp1 * J1;
+            pr[8] = J0 * kj0; pr[9] = J0 * kj1; pr[10] = J1 * kj0; pr[11] = J1 * kj1;
+            pr[12] = J0 * v; pr[13] = J1 * v;
+            pr[14] = J0 * yv0; pr[15] = J0 * yv1; pr[16] = J1 * yv0; pr[17] = J1 * yv1;
+            pr[18] = J0 * vA; pr[19] = J1 * vA;
             {
                 int idx;
                 const double sv = wave_reduce_scatter<NV>(pr, lane, idx);
@@ -725,20 +758,22 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             const V2 e = {o[12], o[13]};
             const Mat2 jy = m2(o[14], o[15], o[16], o[17]);
             const V2 eA = {o[18], o[19]};
-            STAMP3(2);
-            // off-critical dots from helper wave hw 3
+            STAMP4(2);
             lds_wait_ge(ddone, (uint32_t)(i + 1), a.status, dead);
-            STAMP3(3);
+            STAMP4(3);
             const V2 b1 = {dots[0], dots[1]}, b2 = {dots[2], dots[3]};
             const Mat2 f1 = m2(dots[4], dots[5], dots[6], dots[7]);
             const Mat2 f2 = m2(dots[8], dots[9], dots[10], dots[11]);
             const Mat2 ny = m2(dots[12], dots[13], dots[14], dots[15]);
             const V2 b1A = {dots[16], dots[17]}, b2A = {dots[18], dots[19]};
-            // raw y_{i,i-1}
+            // raw y_{i,i-1} from row i's Y window
             double y0 = 0, y1 = 0;
-            if (has_prev) { y0 = (double)yst[(i & 3) * 4 + 0]; y1 = (double)yst[(i & 3) * 4 + 1]; }
+            if (has_prev) {
+                const float2 yy = ywin[(size_t)(i & (kYW - 1)) * 128 + (i - 1 - win_lo(i >> 4))];
+                y0 = (double)yy.x;
+                y1 = (double)yy.y;
+            }
             const double zp0 = r00 * y0 + r01 * y1, zp1 = r10 * y0 + r11 * y1;
-            // ---- 2x2 algebra ----
             const Mat2 JW = add(sub(cc, quad(a1, Mip, a1)), quad(a2, Sip, a2));
             const Mat2 Mm = add(Rm, sym(JW));
             const Mat2 Mi = has_prev ? inv2s(Mm) : m2(0, 0, 0, 0);
@@ -749,7 +784,6 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             const Mat2 JnK = add(sub(ny, quad(f1, Mip, f1)), quad(f2, Sip, f2));
             const Mat2 JnX = sub(JnK, quad(wn, Mi, wn));
             const Mat2 Si = inv2s(sub(Rm, sym(JnX)));
-            // ---- lane-local assembly ----
             const double W0 = kj0 - (Lp0 * a1.a + Lp1 * a1.c) + (Gp0 * a2.a + Gp1 * a2.c);
             const double W1 = kj1 - (Lp0 * a1.b + Lp1 * a1.d) + (Gp0 * a2.b + Gp1 * a2.d);
             const double u = v - (Lp0 * b1.x + Lp1 * b1.y) + (Gp0 * b2.x + Gp1 * b2.y);
@@ -762,13 +796,12 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 const double uA = vA - (Lp0 * b1A.x + Lp1 * b1A.y) + (Gp0 * b2A.x + Gp1 * b2A.y);
                 const V2 s1 = mtv(a1, mv(Mip, b1A)), s2 = mtv(a2, mv(Sip, b2A));
                 const V2 JuA = {eA.x - s1.x + s2.x, eA.y - s1.y + s2.y};
-                // K_i[:, 0:2] (row k) and W_i rows 0, 1 (uniform)
                 const double* r0 = rec + (ppar * D + 0) * 8;
                 const double* r1 = rec + (ppar * D + 1) * 8;
                 const double KE0 = brow[0] - (Lp0 * r0[2] + Lp1 * r0[3]) + (Gp0 * r0[6] + Gp1 * r0[7]);
                 const double KE1 = brow[1] - (Lp0 * r1[2] + Lp1 * r1[3]) + (Gp0 * r1[6] + Gp1 * r1[7]);
-                const double WE00 = __shfl(W0, 0), WE01 = __shfl(W1, 0);   // W row 0
-                const double WE10 = __shfl(W0, 1), WE11 = __shfl(W1, 1);   // W row 1
+                const double WE00 = __shfl(W0, 0), WE01 = __shfl(W1, 0);
+                const double WE10 = __shfl(W0, 1), WE11 = __shfl(W1, 1);
                 const double wz0 = WE00 * zp0 + WE10 * zp1, wz1 = WE01 * zp0 + WE11 * zp1;
                 const double tA = uA + KE0 * zp0 + KE1 * zp1;
                 const V2 jA = {JuA.x + wz0, JuA.y + wz1};
@@ -783,28 +816,27 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             const double Xn0 = kn0 - (Ln0 * wn.a + Ln1 * wn.c);
             const double Xn1 = kn1 - (Ln0 * wn.b + Ln1 * wn.d);
             const double Gn0 = Xn0 * Si.a + Xn1 * Si.c, Gn1 = Xn0 * Si.b + Xn1 * Si.d;
-            STAMP3(4);
-            // naive: diag(P_i) from running sums of squares (own old value removed)
+            STAMP4(4);
             double sq_other = 0.0;
             if (is_naive) {
                 const int src = (k >= 2 && k < 2 + R) ? k + R : ((k >= 2 + R && k < D) ? k - R : k);
                 sq_other = __shfl(ssq_l, src);
             }
-            // ---- publish ----
             if (kl) {
                 const float* xold = xring + (i & 7) * 64;
                 const float mold = xold[k];
                 const float nw = __fadd_rn(__fmul_rn(lr, (float)mus), __fmul_rn(om, mold));
-                xn[(size_t)i * D + k] = nw;
-                const uint64_t gr = ((uint64_t)a.epoch << 32) | (uint64_t)__float_as_uint(nw);
-                gran_store_agent(a.hand + ((size_t)tl * n + i) * D + k, gr);
-                if (tl == TL - 1 && a.halo_out != nullptr)
-                    gran_store_system(a.halo_out + (size_t)i * D + k, gr);
+                // LDS copies first: the helpers of the next step read them
                 mu32[par * D + k] = nw;
                 mu64[par * D + k] = (double)nw;
                 double* rc = rec + (par * D + k) * 8;
                 rc[0] = Ln0; rc[1] = Ln1; rc[2] = W0; rc[3] = W1;
                 rc[4] = Gn0; rc[5] = Gn1; rc[6] = Xn0; rc[7] = Xn1;
+                xn[(size_t)i * D + k] = nw;
+                const uint64_t gr = ((uint64_t)a.epoch << 32) | (uint64_t)__float_as_uint(nw);
+                gran_store_agent(a.hand + ((size_t)tl * n + i) * D + k, gr);
+                if (tl == TL - 1 && a.halo_out != nullptr)
+                    gran_store_system(a.halo_out + (size_t)i * D + k, gr);
                 if (is_naive) {
                     const double p = r00, s = r11;
                     double pd;
@@ -822,26 +854,29 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             Wp0 = W0; Wp1 = W1; Xp0 = Xn0; Xp1 = Xn1; Lp0 = Ln0; Lp1 = Ln1; Gp0 = Gn0; Gp1 = Gn1;
             Mip = Mi;
             Sip = Si;
-            STAMP3(5);
-            // next base rows, once every helper wave has written K_i
+            STAMP4(5);
             lds_wait_ge(kcnt, 7u * (uint32_t)(i + 1), a.status, dead);
-            STAMP3(6);
+            STAMP4(6);
             const double* Kn = Kbuf + (size_t)ppar * DD;
             if (kl) {
 #pragma unroll
                 for (int c = 0; c < D; ++c) brow[c] = Kn[(size_t)k * D + c];
             }
-            STAMP3(7);
+            STAMP4(7);
             lds_barrier3();
         }
         {
             const int i = n;
-            PROG3();
+            PROG4();
         }
-        lds_barrier3();   // epilogue step n
+        lds_barrier3();
     } else {
         // ============================ HELPERS ============================
-        int lk[LTQ], lm[LTQ];
+        // HBK lanes (hw 0..5): entries of the K rebuild; HBC lanes (hw 3..5): entries of
+        // the covariance output, stored after the wave's GEMM loads are issued (vmcnt
+        // retires in order: stores ahead of those loads would delay the next GEMM part).
+        constexpr int NHC = 192, LTQC = (NLT + NHC - 1) / NHC;
+        int lk[LTQ], lm[LTQ], ck[LTQC], cm[LTQC];
 #pragma unroll
         for (int q = 0; q < LTQ; ++q) {
             const int e = hl + C::NHB * q;
@@ -850,13 +885,24 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             lk[q] = k;
             lm[q] = m;
         }
+#pragma unroll
+        for (int q = 0; q < LTQC; ++q) {
+            const int e = (tid - 256) + NHC * q;
+            int k = -1, m = -1;
+            if (hw >= 3 && hw <= 5 && e < NLT) tri_decode3(e, k, m);
+            ck[q] = k;
+            cm[q] = m;
+        }
+        // static priority: HF1 (hw 0..2) and HX (hw 6) feed the solver's next step
+        if (hw <= 2 || hw == 6) __builtin_amdgcn_s_setprio(2);
         for (int i = 0; i <= n; ++i) {
-            STAMP3(0);
+            STAMP4(0);
             const int par = i & 1, ppar = (i + 1) & 1;
-            const double* Bi = Kbuf + (size_t)par * DD;      // B_i
-            double* Kn = Kbuf + (size_t)ppar * DD;           // K_i = B_{i+1}
-            // HX (hw 5, off the solver's SIMD): dots that do not involve mu_{i-1}
-            if (hw == 5 && i < n) {
+            const double* Bi = Kbuf + (size_t)par * DD;
+            double* Kn = Kbuf + (size_t)ppar * DD;
+            const double* rp = rec + (size_t)ppar * D * 8;
+            // HX (hw 6): dots that do not involve mu_{i-1} (the solver waits for them)
+            if (hw == 6 && i < n) {
                 const int k = lane;
                 const int kc = (k < D) ? k : 0;
                 const double msk = (k < D) ? 1.0 : 0.0;
@@ -868,34 +914,111 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 jcol<R>(xring + ((i + 1) & 7) * 64, i + 1 < n, kc, n0, n1);
                 const double gA = (k < 2) ? g : 0.0;
                 double pr[20];
-                pr[0] = W0 * g; pr[1] = W1 * g; pr[2] = X0 * g; pr[3] = X1 * g;           // b1, b2
-                pr[4] = W0 * n0; pr[5] = W0 * n1; pr[6] = W1 * n0; pr[7] = W1 * n1;       // f1[p][q]
-                pr[8] = X0 * n0; pr[9] = X0 * n1; pr[10] = X1 * n0; pr[11] = X1 * n1;     // f2[p][q]
-                pr[12] = msk * n0 * yv0; pr[13] = msk * n0 * yv1;                          // ny[q][p]
+                pr[0] = W0 * g; pr[1] = W1 * g; pr[2] = X0 * g; pr[3] = X1 * g;
+                pr[4] = W0 * n0; pr[5] = W0 * n1; pr[6] = W1 * n0; pr[7] = W1 * n1;
+                pr[8] = X0 * n0; pr[9] = X0 * n1; pr[10] = X1 * n0; pr[11] = X1 * n1;
+                pr[12] = msk * n0 * yv0; pr[13] = msk * n0 * yv1;
                 pr[14] = msk * n1 * yv0; pr[15] = msk * n1 * yv1;
-                pr[16] = W0 * gA; pr[17] = W1 * gA; pr[18] = X0 * gA; pr[19] = X1 * gA;   // b1A, b2A
+                pr[16] = W0 * gA; pr[17] = W1 * gA; pr[18] = X0 * gA; pr[19] = X1 * gA;
                 int idx;
                 const double sv = wave_reduce_scatter<20>(pr, lane, idx);
                 if (idx < 20) dots[idx] = sv;
                 if (lane == 0) lds_signal_set(ddone, (uint32_t)(i + 1));
-                STAMP3(1);
+                STAMP4(1);
             }
-            // HB (hw 0..5): K_i = B_i - L W^T + G X^T, fused covariance of node i-1
-            if (hw <= 5) {
-                const double* rp = rec + (size_t)ppar * D * 8;
-                const double* pdp = pdl + (size_t)ppar * D;
-                const float* co = cring + (size_t)((i + 3) & 3) * LY::cs;   // node i-1
-                float* cv = cvw + (size_t)(i > 0 ? i - 1 : 0) * DD;
+            // ring + transposed copy of node i-1's new (U, V)  (hw 4).  The wave's
+            // stores of the previous step are drained first (a step old: free), so
+            // that Mt store is visible to loads issued after this step's barrier.
+            if (hw == 4) {
+#ifndef AME_S4_EAGER_DRAIN
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+                if (i >= 1 && lane < M2) {
+                    const float vnew = mu32[ppar * D + 2 + lane];
+                    mring[((i - 1) & (kMR - 1)) * 64 + lane] = vnew;
+                    Mt[(size_t)lane * ns + (i - 1)] = vnew;
+                }
+            }
+            // HBK (hw 0..5): K_i = B_i - L W^T + G X^T  (LDS only)
+            if (hw <= 5 && i < n) {
 #pragma unroll
                 for (int q = 0; q < LTQ; ++q) {
-                    const bool ok = lk[q] >= 0;
-                    const int k = ok ? lk[q] : 0, m = ok ? lm[q] : 0;
+                    if (lk[q] < 0) continue;
+                    const int k = lk[q], m = lm[q];
                     const double* rk = rp + k * 8;
                     const double* rm = rp + m * 8;
-                    const double bkm = Bi[k * D + m];
-                    const float ckm = co[k * D + m], cmk = co[m * D + k];
-                    const double c = bkm - (rk[0] * rm[2] + rk[1] * rm[3]);
+                    const double c = Bi[k * D + m] - (rk[0] * rm[2] + rk[1] * rm[3]);
                     const double kn = c + (rk[4] * rm[6] + rk[5] * rm[7]);
+                    Kn[k * D + m] = kn;
+                    Kn[m * D + k] = kn;
+                }
+            }
+            STAMP4(4);
+            if (lane == 0) lds_signal_add(kcnt, 1u);
+            // HF1 (hw 0..2): hand-off of mu_{i+1,t-1}, AR terms, g_{i+1}
+            if (hw <= 2 && i + 1 < n) {
+                uint64_t gv = 0;
+                if (lane < D) gv = pring[(size_t)((i + 1) & 3) * 128 + lane];
+                gran_finish(i + 1, gv, muL + hw * 64);
+                STAMP4(2);
+                wave_lds_sync3();
+                hf1(i + 1);
+                STAMP4(3);
+                if (hw == 0) jn_fill(i + 2);
+                if (lane == 0) lds_signal_add(gcnt, 1u);
+            }
+            if (i < n) {
+                // block GEMM (hw 0..3): this step's part, then the loads of the next
+#ifndef AME_S4_ABL_GEMM
+                if (hw <= 3) {
+#else
+                if (false) {
+#endif
+                    const int bq = i + kGS;
+                    if ((bq >> 4) >= 2) gemm_compute(bq >> 4, bq & 15);
+                    const int bq1 = bq + 1;
+                    if ((bq1 >> 4) >= 2 && i + 1 < n) gemm_load(bq1 >> 4, bq1 & 15);
+                }
+                // window GEMV of node i+2 (hw 4, 5: one half each)
+#ifndef AME_S4_ABL_WIN
+                if ((hw == 4 || hw == 5) && i + 2 < n) wgemv(i + 2, hw - 4);
+#endif
+                STAMP4(5);
+                if (hw == 6) {
+                    // loader: Y window row i+5, covariance of node i+2, old means of
+                    // node i+5 (slice t) and i+4 (slice t+1), granules of node i+4,
+                    // old (U, V) of node i+22
+                    dma_yw(i + 5);
+                    dma_cov(i + 2);
+                    dma_x(i + 5);
+                    dma_r(i + 4);
+                    dma_p(i + 4);
+                    dma_m(i + kGL);
+                    // block reduction: block (i+2)/16 finished its GEMM last step
+                    if (((i + kGS) & 15) == 0) {
+                        const int bb = (i + 2) >> 4;
+                        if (bb >= 2 && kBS * bb < n) gemm_reduce(bb);
+                    }
+                    STAMP4(6);
+                }
+            }
+            // HBC (hw 3..5): damped covariance of node i-1,
+            // P_{i-1}^-1 = B_i - L_{i-1} W_{i-1}^T  (+ bad mask, jitter; naive: diag)
+#ifndef AME_S4_ABL_HBC
+            if (hw >= 3 && hw <= 5 && i >= 1) {
+#else
+            if (false) {
+#endif
+                const double* pdp = pdl + (size_t)ppar * D;
+                const float* co = cring + (size_t)((i + 3) & 3) * LY::cs;   // node i-1
+                float* cv = cvw + (size_t)(i - 1) * DD;
+#pragma unroll
+                for (int q = 0; q < LTQC; ++q) {
+                    if (ck[q] < 0) continue;
+                    const int k = ck[q], m = cm[q];
+                    const double* rk = rp + k * 8;
+                    const double* rm = rp + m * 8;
+                    const double c = Bi[k * D + m] - (rk[0] * rm[2] + rk[1] * rm[3]);
                     float c32;
                     if (is_naive) {
                         c32 = (k == m) ? 1.0f / ((float)pdp[k] + 1e-8f) : 0.f;
@@ -904,84 +1027,26 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                         if (is_bad && ((k < 2) != (m < 2))) c32 = 0.f;
                         if (k == m) c32 = c32 + 1e-6f;
                     }
-                    const float n_km = __fadd_rn(__fmul_rn(lr, c32), __fmul_rn(om, ckm));
-                    const float n_mk = __fadd_rn(__fmul_rn(lr, c32), __fmul_rn(om, cmk));
-                    if (ok && i < n) {
-                        Kn[k * D + m] = kn;
-                        Kn[m * D + k] = kn;
-                    }
-                    if (ok && i >= 1) {
-                        cv[k * D + m] = n_km;
-                        if (k != m) cv[m * D + k] = n_mk;
-                    }
+                    cv[k * D + m] = __fadd_rn(__fmul_rn(lr, c32), __fmul_rn(om, co[k * D + m]));
+                    if (k != m) cv[m * D + k] = __fadd_rn(__fmul_rn(lr, c32), __fmul_rn(om, co[m * D + k]));
                 }
             }
-            STAMP3(4);
-            if (lane == 0) lds_signal_add(kcnt, 1u);
-            // HF1 (hw 0..2): hand-off of mu_{i+1,t-1} (DMA'd 3 steps ago), AR terms, g_{i+1}
-            if (hw <= 2 && i + 1 < n) {
-                uint64_t gv = 0;
-                if (lane < D) gv = pring[(size_t)((i + 1) & 3) * 128 + lane];
-                gran_finish(i + 1, gv, muL + hw * 64);
-                STAMP3(2);
-                wave_lds_sync3();
-                hf1(i + 1);
-                STAMP3(3);
-                if (hw == 0) jn_fill(i + 2);   // J rows of node i+2 for HF2
-                if (lane == 0) lds_signal_add(gcnt, 1u);
+            if (i < n && hw >= 3 && i + 1 < n) {
+                lds_wait_ge(kcnt, 7u * (uint32_t)(i + 1), a.status, dead);
+                lds_wait_ge(gcnt, 3u * (uint32_t)(i + 1), a.status, dead);
+                STAMP4(7);
+                hf2(i + 1, Kn);
+                STAMP4(8);
             }
-            if (i < n) {
-                // M update with mu_{i-1} (owner lane)
-                if (i >= 1) {
-                    const int j = i - 1, so = j / kNH, ho = j - so * kNH;
-                    if (hl == ho) {
-                        const float* mup = mu32 + ppar * D;
-                        if (so < NSREG) {
-#pragma unroll
-                            for (int s = 0; s < NSREG; ++s)
-                                if (s == so) {
-#pragma unroll
-                                    for (int c = 0; c < M2; ++c) mreg[s][c] = mup[2 + c];
-                                }
-                        } else {
-                            for (int c2 = 0; c2 < MP; ++c2) {
-                                float2 v = make_float2(mup[2 + 2 * c2], 0.f);
-                                if (2 * c2 + 1 < M2) v.y = mup[3 + 2 * c2];
-                                mlds[((so - NSREG) * MP + c2) * kNH + hl] = v;
-                            }
-                        }
-                    }
-                }
-                // HE: GEMV of node i+2 (its Y row landed in the ring by step i-1)
-                if (i + 2 < n) gemv(i + 2, yring + (size_t)((i + 2) & 3) * YS);
-                STAMP3(5);
-                // loader: this step's batch -- Y row i+5, covariance of node i+2, old
-                // means of node i+5 (slice t) and i+4 (slice t+1), granules of node i+4
-                if (hw == 6) {
-                    dma_y(i + 5);
-                    dma_cov(i + 2);
-                    dma_x(i + 5);
-                    dma_r(i + 4);
-                    dma_p(i + 4);
-                    STAMP3(6);
-                }
-                // HF2 (hw 3..6): v_{i+1}, yv_{i+1} with K_i
-                if (hw >= 3 && i + 1 < n) {
-                    lds_wait_ge(kcnt, 7u * (uint32_t)(i + 1), a.status, dead);
-                    lds_wait_ge(gcnt, 3u * (uint32_t)(i + 1), a.status, dead);
-                    STAMP3(7);
-                    hf2(i + 1, Kn);
-                    STAMP3(8);
-                }
-            }
-            // the batch issued 2 steps ago must have landed before the next step reads it
             if (hw == 6) vm_wait_le(2 * KDMA);
-            STAMP3(9);
+#ifdef AME_S4_EAGER_DRAIN
+            if (hw == 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+            STAMP4(9);
             lds_barrier3();
         }
     }
-    // ---- slice done: release its means, covariances and granules, then flag it
-    // for the next sweep (every wave drains its own stores first) ----
+    // ---- slice done: release, flag (as v3) ----
     if (a.done != nullptr) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -991,8 +1056,6 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             __hip_atomic_store(a.done + tl, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    // ---- first slice of a rank with a left neighbour: its new means are that
-    // rank's next_old in the next (pipelined) sweep; system-scope release ----
     if (tl == 0 && a.back_out != nullptr) {
         for (int e = tid; e < n * D; e += kNT)
             a.back_out[e] = __uint_as_float(__hip_atomic_load(
@@ -1009,51 +1072,41 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     }
 }
 
-
-// v3 keeps one state row per solver lane: D = 2 + 2r <= 64.
-constexpr int kV3MaxR = 31;
+// v4 covers r <= 16 (one 16-column MFMA tile per GEMM), n % 4 == 0, 8 <= n <= 2048.
+template <int R>
+static int sweep4_fits(int n) {
+    if (R > 16 || n < 8 || (n & 3) != 0 || n > 64 * 16 * kVM) return 0;
+    using C = Cfg4<R>;
+    if (2 * (C::NC + 5) > 63) return 0;
+    return Lay4<R>::total <= kLDSMAX;
+}
 
 template <int R>
-static int l3_total(int n) { return Lay<R>::total(n, Cfg<R>::NSREG); }
-
-template <int R>
-static int sweep3_occupancy(int n) {
-    const int lds = l3_total<R>(n);
-    auto kern = ame_sweep3_kernel<R>;
-    if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
-        hipSuccess)
+static int sweep4_occupancy() {
+    const int lds = Lay4<R>::total;
+    auto kern = ame_sweep4_kernel<R>;
+    if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
         return 0;
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kNT, (size_t)lds) != hipSuccess)
-        return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kNT, (size_t)lds) != hipSuccess) return 0;
     return per_cu;
 }
 
-int ame_sweep3_blocks_per_cu(int n, int r) {
+int ame_sweep4_supported(int n, int r) {
     switch (r) {
 #define X(RR) \
-    case RR: if constexpr (RR <= kV3MaxR) return sweep3_occupancy<RR>(n); else return 0;
+    case RR: if constexpr (RR <= 16) return sweep4_fits<RR>(n); else return 0;
         AME_FOR_EACH_R(X)
 #undef X
         default: return 0;
     }
 }
 
-// v3 needs: the slice's LDS (rings + overflow node slots) within one CU, at
-// most 2 x 31 loader DMA instructions in flight (vmcnt range) and D <= 64.
-template <int R>
-static int sweep3_fits(int n) {
-    using C = Cfg<R>;
-    if (n < 2 || C::D > 64) return 0;
-    const int ny = (n * 8 + 1023) / 1024;
-    if (2 * (ny + C::NC + 3) > 63) return 0;
-    return l3_total<R>(n) <= kLDSMAX;
-}
-
-int ame_sweep3_supported(int n, int r) {
+int ame_sweep4_blocks_per_cu(int n, int r) {
+    (void)n;
     switch (r) {
 #define X(RR) \
-    case RR: if constexpr (RR <= kV3MaxR) return sweep3_fits<RR>(n); else return 0;
+    case RR: if constexpr (RR <= 16) return sweep4_occupancy<RR>(); else return 0;
         AME_FOR_EACH_R(X)
 #undef X
         default: return 0;
@@ -1061,27 +1114,27 @@ int ame_sweep3_supported(int n, int r) {
 }
 
 template <int R>
-static int launch_sweep3(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {
-    const int lds = l3_total<R>(dm->n);
-    auto kern = ame_sweep3_kernel<R>;
-    if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
-        hipSuccess)
+static int launch_sweep4(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {
+    const int lds = Lay4<R>::total;
+    auto kern = ame_sweep4_kernel<R>;
+    if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
         return -2;
     hipLaunchKernelGGL(kern, dim3(dm->T_local), dim3(kNT), (size_t)lds, st, *dm, *a);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-int ame_sweep3_dispatch(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {
+int ame_sweep4_dispatch(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {
     switch (dm->r) {
 #define X(RR) \
-    case RR: if constexpr (RR <= kV3MaxR) return launch_sweep3<RR>(dm, a, st); else return -1;
+    case RR: if constexpr (RR <= 16) return launch_sweep4<RR>(dm, a, st); else return -1;
         AME_FOR_EACH_R(X)
 #undef X
         default: return -1;
     }
 }
 
-long long ame_sweep3_work_doubles(const ame_dims* dm) {
-    (void)dm;   // the base inverse lives in LDS (formed in the sweep prologue)
-    return 0;
+// the transposed (U, V) copy: [T_local][2r][roundup(n, 16)] fp32, in doubles
+long long ame_sweep4_work_doubles(const ame_dims* dm) {
+    const long long ns = (dm->n + 15) & ~15;
+    return ((long long)dm->T_local * 2 * dm->r * ns + 1) / 2;
 }

@@ -122,6 +122,27 @@ def assemble(out, n, T, d, variant, C: Constants):
             "elbo": loglik + prior0 + trans + ent, "recon": recon}
 
 
+def slice_groups(T_local: int, max_slices: int, force: int = 0):
+    """Consecutive groups [(offset, size)] of the local slices that each fit on
+    the chip at once (a sweep's slices spin on each other, so all slices of one
+    launch must be co-resident).  The groups of one sweep run one after another
+    on one stream; group g+1's first slice takes slice (g's last)'s new means
+    from the hand-off granules group g left behind, so the Gauss-Seidel order
+    is the same as one launch over all slices (reference: the t loop of
+    structured_mf.py:240 has no limit on T)."""
+    cap = max_slices if force <= 0 else min(force, max_slices)
+    if cap < 1:
+        raise RuntimeError("ame_amd: no sweep workgroup fits on this device")
+    k = -(-T_local // cap)
+    base, extra = divmod(T_local, k)
+    out, off = [], 0
+    for g in range(k):
+        sz = base + (1 if g < extra else 0)
+        out.append((off, sz))
+        off += sz
+    return out
+
+
 class DeviceEngine:
     """HBM-resident state of one VI run on one GPU (one time shard)."""
 
@@ -173,10 +194,10 @@ class DeviceEngine:
             self.status = torch.zeros(1, dtype=torch.int32, device=dev)
         self.epoch = 0
         self.max_slices = int(self.L.ame_sweep_max_slices(self.n, self.r))
-        if sh.T_local > self.max_slices:
-            raise RuntimeError(
-                f"ame_amd: {sh.T_local} time slices per GPU exceed the co-resident sweep "
-                f"lanes ({self.max_slices}) for n={self.n}, r={self.r}; shard over more GPUs")
+        if self.max_slices < 1:
+            raise RuntimeError(f"ame_amd: no sweep kernel fits n={self.n}, r={self.r}")
+        self.groups = slice_groups(sh.T_local, self.max_slices,
+                                   int(os.environ.get("AME_SLICE_GROUP", "0")))
         self._out_host = None
         self._out_valid = False
         self.timing = False       # record HIP events around each kernel launch
@@ -187,6 +208,7 @@ class DeviceEngine:
         self.sweep_streams = [torch.cuda.Stream(device=self.dev, priority=-1) for _ in range(2)]
         self.done = torch.zeros(max(sh.T_local, 1), dtype=torch.int32, device=self.dev)
         self.pipelined = (bool(self.L.ame_sweep_orders_slices(self.n, self.r))
+                          and len(self.groups) == 1
                           and 2 * sh.T_local <= self.max_slices
                           and os.environ.get("AME_PIPELINE", "1") != "0")
         if self.halo is not None:   # every rank must take the same path
@@ -295,16 +317,29 @@ class DeviceEngine:
             stream.wait_event(ready)
             if self._specs:   # its input slot is the output of the last queued sweep
                 stream.wait_event(self._specs[-1][0])
-        a = _lib.ame_sweep_args(
-            Yt=_ptr(self.Yt), x_old=_ptr(self.xs[src]), x_new=_ptr(self.xs[dst]), next_old=next_old,
-            hand=_ptr(self.hand), halo_in=halo_in, halo_out=halo_out, cov=_ptr(self.covs[src]),
-            consts=_ptr(self.consts), rinv=self.C.rinv4(), lr=self.lr,
-            one_minus_lr=float(1.0 - self.lr), epoch=self.epoch, status=_ptr(self.status),
-            work=_ptr(self.sweep_work), cov_new=_ptr(self.covs[dst]), done=_ptr(self.done),
-            wait_epoch=wait, back_out=back_out, back_in=back_in)
         tok = self._tic("sweep", stream)
-        _lib.check(self.L.ame_sweep(ctypes.byref(self.dims), ctypes.byref(a),
-                                    ctypes.c_void_p(stream.cuda_stream)), "ame_sweep")
+        n, d, sh = self.n, self.d, self.shard
+        last = len(self.groups) - 1
+        for g, (off, size) in enumerate(self.groups):
+            def at(t, slices, per_slice, esize):   # pointer to local slice `slices` of t
+                return ctypes.c_void_p(t.data_ptr() + slices * per_slice * esize)
+            nd, ndd, nn2 = n * d, n * d * d, n * n * 2
+            g_halo_in = halo_in if g == 0 else at(self.hand, off - 1, nd, 8)
+            g_halo_out = halo_out if g == last else None
+            g_next_old = next_old if g == last else at(self.xs[src], off + size, nd, 4)
+            dims = _lib.ame_dims(n, self.r, size, sh.t_begin + off, sh.T_total, self.vcode)
+            a = _lib.ame_sweep_args(
+                Yt=at(self.Yt, off, nn2, 4), x_old=at(self.xs[src], off, nd, 4),
+                x_new=at(self.xs[dst], off, nd, 4), next_old=g_next_old,
+                hand=at(self.hand, off, nd, 8), halo_in=g_halo_in, halo_out=g_halo_out,
+                cov=at(self.covs[src], off, ndd, 4), consts=_ptr(self.consts),
+                rinv=self.C.rinv4(), lr=self.lr, one_minus_lr=float(1.0 - self.lr),
+                epoch=self.epoch, status=_ptr(self.status), work=_ptr(self.sweep_work),
+                cov_new=at(self.covs[dst], off, ndd, 4), done=at(self.done, off, 1, 4),
+                wait_epoch=wait, back_out=back_out if g == 0 else None,
+                back_in=back_in if g == last else None)
+            _lib.check(self.L.ame_sweep(ctypes.byref(dims), ctypes.byref(a),
+                                        ctypes.c_void_p(stream.cuda_stream)), "ame_sweep")
         self._toc(tok)
         done = torch.cuda.Event()
         done.record(stream)

@@ -184,3 +184,64 @@ def test_config4_rank_shape_two_ranks(gpu_device):
     assert dig_d == dig_s
     assert np.allclose(elbo_d, elbo_s, rtol=1e-6, atol=0)
     assert np.allclose(rec_d, rec_s, rtol=1e-12, atol=0)
+
+
+# ---------------- config 4 on one GPU: T=512 > co-resident slices ----------------
+def _c4full_run(distributed, group):
+    os.environ["AME_SLICE_GROUP"] = group
+    from ame_amd import TemporalAMEModel
+    dev = torch.device("cuda", 0)
+    m = TemporalAMEModel(1024, 512, 16, seed=42)
+    m.generate_data_fast(device=dev, seed=42)
+    vi = _vi(m, "good", 0.01, dev, distributed=distributed)
+    groups = len(vi.engine.groups)
+    h = vi.fit(max_iter=2, tolerance=0.0, verbose=False)
+    mean = vi.X_mean.numpy().copy()
+    digest = hashlib.sha256(vi.X_cov.numpy().tobytes()).hexdigest()
+    return mean, digest, [float(e) for e in h["elbo"]], list(h["reconstruction_error"]), groups
+
+
+def _c4full_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = _c4full_run(True, "128")   # two groups per rank: both ranks fit on the chip
+        if rank == 0:
+            q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_config4_full_T_one_gpu(gpu_device):
+    """BASELINE config 4 (n=1024, T=512, r=16) in one process on one GPU: the
+    512 slices exceed the co-resident workgroups, so each sweep runs as
+    consecutive slice groups; bit-equal to the same problem split over two
+    time-sharded ranks."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_c4full_worker, args=(rk, 2, port, q)) for rk in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        result = q.get(timeout=200)
+    except Exception:
+        result = None
+    for p in procs:
+        p.join(timeout=30)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.exitcode is None:
+            p.kill()
+            p.join()
+    assert codes == [0, 0], f"rank exit codes {codes}"
+    mean_d, dig_d, elbo_d, rec_d, groups_d = result
+    mean_s, dig_s, elbo_s, rec_s, groups_s = _c4full_run(False, "0")
+    os.environ.pop("AME_SLICE_GROUP", None)
+    assert groups_s >= 2 and groups_d == 2
+    assert np.array_equal(mean_d, mean_s)
+    assert dig_d == dig_s
+    assert np.allclose(elbo_d, elbo_s, rtol=1e-6, atol=0)
+    assert np.allclose(rec_d, rec_s, rtol=1e-12, atol=0)

@@ -298,3 +298,23 @@ def test_state_attributes_stay_live(gpu_device):
     X[0, 0, 0] += 1.0                      # host edit -> uploaded before the next step
     vi.fit(max_iter=1, tolerance=0.0, verbose=False)
     assert vi.engine.x_a.shape[1] == 40
+
+
+@pytest.mark.parametrize("group", ["3", "4"])
+def test_slice_groups_are_exact(group, gpu_device, monkeypatch):
+    """Local slices launched as consecutive groups (AME_SLICE_GROUP forces the
+    size; by default only when T_local exceeds the co-resident workgroups):
+    bit-identical to one launch over all slices."""
+    from ame_amd import TemporalAMEModel
+    outs = []
+    for g in ("0", group):
+        monkeypatch.setenv("AME_SLICE_GROUP", g)
+        m = TemporalAMEModel(48, 10, 3, seed=12)
+        m.generate_data_fast(seed=12)
+        vi = _vi(m, "good", 0.5, gpu_device)
+        assert len(vi.engine.groups) == (1 if g == "0" else -(-10 // int(g)))
+        h = vi.fit(max_iter=3, tolerance=0.0, verbose=False)
+        outs.append((vi.X_mean.numpy().copy(), vi.X_cov.numpy().copy(), [float(e) for e in h["elbo"]]))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.array_equal(outs[0][1], outs[1][1])
+    assert outs[0][2] == outs[1][2]

@@ -1,7 +1,7 @@
-"""Diagnostic for the v3 sweep (ame_sweep3.hip): in-kernel s_memtime stamps.
+"""Diagnostic for the v4 sweep (ame_sweep4.hip): in-kernel s_memtime stamps.
 
-    python tools/sweep3_stamps.py --build      # here: hipcc -DAME_STAMPS -> _build/libame_amd_stamps3.so
-    python tools/sweep3_stamps.py              # GPU box: config-3 sweeps, print per-wave timelines
+    python tools/sweep4_stamps.py --build      # here: hipcc -DAME_STAMPS -> _build/libame_amd_stamps4.so
+    python tools/sweep4_stamps.py              # GPU box: config-3 sweeps, per-wave step timelines
 
 The stamped build's run time is never quoted; only its shares / timelines.
 """
@@ -16,16 +16,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "python-temporal-ame-svi_amd")
 BDIR = os.path.join(PKG, "ame_amd", "_build")
 TAG = ([a.split("=", 1)[1] for a in sys.argv if a.startswith("--tag=")] or [""])[0]
-SO = os.path.join(BDIR, f"libame_amd_stamps3{TAG}.so")
-SRCS = ("ame_sweep.hip", "ame_sweep3.hip", "ame_sweep4.hip", "ame_cov.hip", "ame_elbo.hip", "ame_capi.hip",
-        "ame_selftest.hip", "ame_align.hip")
+SO = os.path.join(BDIR, f"libame_amd_stamps4{TAG}.so")
+SRCS = ("ame_sweep.hip", "ame_sweep3.hip", "ame_sweep4.hip", "ame_cov.hip", "ame_elbo.hip",
+        "ame_capi.hip", "ame_selftest.hip", "ame_align.hip")
 NAMES = {
     0: ["start", "J+kj", "reduce", "ddone", "2x2+assembly", "publish", "kcnt", "brow"],
-    1: ["start", "-", "poll", "hf1", "HB", "GEMV", "-", "-", "-", "end"],
-    2: ["start", "HX", "-", "-", "HB", "GEMV", "-", "kcnt", "hf2", "end"],
-    3: ["start", "-", "-", "-", "(no HB)", "GEMV", "DMA", "kcnt", "hf2", "vmwait"],
+    1: ["start", "-", "poll", "hf1", "HBK", "GEMM", "-", "-", "-", "end"],
+    2: ["start", "-", "-", "-", "HBK", "GEMM", "-", "kcnt+gcnt", "hf2", "end"],
+    3: ["start", "-", "-", "-", "HBK", "window", "-", "HBC+kcnt+gcnt", "hf2", "end"],
+    4: ["start", "HX", "-", "-", "(no HB)", "-", "DMA+reduce", "kcnt+gcnt", "hf2", "vmwait"],
 }
-WAVES = ["solver(w0)", "hw0(w1)", "hw5(w6)", "hw6(w7)"]
+WAVES = ["solver(w0)", "hw0(w1)", "hw3(w4)", "hw4(w5)", "hw6(w7)"]
 
 
 def build(r=16):
@@ -35,7 +36,7 @@ def build(r=16):
         "--defs=", "")).split(",") if d]
     objs = []
     for src in SRCS:
-        o = os.path.join(BDIR, src.replace(".hip", f"_s3{TAG}.o"))
+        o = os.path.join(BDIR, src.replace(".hip", f"_s4{TAG}.o"))
         subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC",
                                "-std=c++17", "-DAME_STAMPS", f"-DAME_ONLY_R={r}", *defs,
                                "-Wno-pass-failed", "-c", os.path.join(csrc, src), "-o", o])
@@ -47,6 +48,7 @@ def build(r=16):
 
 def run():
     os.environ["AME_LIB_PATH"] = SO
+    os.environ["AME_SWEEP_V4"] = "1"
     sys.path.insert(0, PKG)
     import torch
     from ame_amd import TemporalAMEModel, TemporalAMEStructuredMFVI
@@ -58,20 +60,14 @@ def run():
     vi.fit(max_iter=2, tolerance=0.0, verbose=False)
     torch.cuda.synchronize()
     L = _lib.lib()
-    L.ame_debug_read_stamps3.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-    st = np.zeros(4 * 16 * 16, dtype=np.uint64)
+    L.ame_debug_read_stamps4.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    st = np.zeros(5 * 16 * 16, dtype=np.uint64)
     pg = np.zeros(256 * 5, dtype=np.uint64)
-    assert L.ame_debug_read_stamps3(st.ctypes.data, pg.ctypes.data) == 0
-    st = st.reshape(4, 16, 16).astype(np.int64)
-    L.ame_debug_read_hwid3.argtypes = [ctypes.c_void_p]
-    hw = np.zeros(8, dtype=np.uint32)
-    L.ame_debug_read_hwid3(hw.ctypes.data)
-    print("HW_ID per wave (wave_id, simd_id, cu_id):",
-          [(int(h & 15), int((h >> 4) & 3), int((h >> 8) & 15)) for h in hw])
+    assert L.ame_debug_read_stamps4(st.ctypes.data, pg.ctypes.data) == 0
+    st = st.reshape(5, 16, 16).astype(np.int64)
     pg = pg.reshape(256, 5).astype(np.int64)[:128]
-    t0 = st[0, :, 0].min()
     print("step period (solver start-to-start), cycles:", np.diff(st[0, :, 0])[:15].tolist())
-    for w in range(4):
+    for w in range(5):
         print(f"--- {WAVES[w]} (cycles after solver step start, median over 16 steps)")
         rel = st[w] - st[0, :, 0][:, None]
         for sl, nm in enumerate(NAMES[w]):
