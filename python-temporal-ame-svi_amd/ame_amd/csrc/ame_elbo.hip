@@ -76,7 +76,7 @@ int ame_pack_dispatch(const float* Y, float* Yt, const ame_dims* dm, unsigned lo
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <int R>
-__global__ void __launch_bounds__(AME_NT)
+__global__ void __launch_bounds__(AME_NT, (R <= 16) ? 4 : 2)   // r <= 16: 4 waves / SIMD, all strips resident
 ame_pairs_kernel(ame_dims dm, const float* __restrict__ Yt, const float* __restrict__ x,
                  double r00, double r01, double r10, double r11, int swap_mode,
                  double* __restrict__ partial) {
@@ -99,20 +99,45 @@ ame_pairs_kernel(ame_dims dm, const float* __restrict__ Yt, const float* __restr
     const float* ys = Yt + (size_t)tl * n * n * 2;
     const float p = (float)r00, q01 = (float)r01, q10 = (float)r10, sr = (float)r11;
 
-    auto stage = [&](int J, int buf) {
+    // staging of a column tile's U, V, a, b: global loads into registers first
+    // (issued a tile ahead), LDS stores after the current tile's compute
+    constexpr int SQ = (AME_TILE * RP + AME_NT - 1) / AME_NT;
+    float su[SQ], sv[SQ], sa = 0.f, sb = 0.f;
+    auto stage_load = [&](int J) {
         const int J0 = J * AME_TILE;
-        for (int idx = threadIdx.x; idx < AME_TILE * RP; idx += AME_NT) {
+#pragma unroll
+        for (int q = 0; q < SQ; ++q) {
+            const int idx = threadIdx.x + AME_NT * q;
             const int row = idx / RP, k = idx - row * RP;
             const int jj = J0 + row;
-            const bool ok = k < R && jj < n;
-            UJ[buf][row * LD + k] = ok ? xs[(size_t)jj * D + 2 + k] : 0.f;
-            VJ[buf][row * LD + k] = ok ? xs[(size_t)jj * D + 2 + R + k] : 0.f;
+            const bool ok = idx < AME_TILE * RP && k < R && jj < n;
+            su[q] = ok ? xs[(size_t)jj * D + 2 + k] : 0.f;
+            sv[q] = ok ? xs[(size_t)jj * D + 2 + R + k] : 0.f;
         }
         if (threadIdx.x < AME_TILE) {
             const int jj = J0 + threadIdx.x;
-            aJ[buf][threadIdx.x] = jj < n ? xs[(size_t)jj * D + 0] : 0.f;
-            bJ[buf][threadIdx.x] = jj < n ? xs[(size_t)jj * D + 1] : 0.f;
+            sa = jj < n ? xs[(size_t)jj * D + 0] : 0.f;
+            sb = jj < n ? xs[(size_t)jj * D + 1] : 0.f;
         }
+    };
+    auto stage_store = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < SQ; ++q) {
+            const int idx = threadIdx.x + AME_NT * q;
+            if (idx < AME_TILE * RP) {
+                const int row = idx / RP, k = idx - row * RP;
+                UJ[buf][row * LD + k] = su[q];
+                VJ[buf][row * LD + k] = sv[q];
+            }
+        }
+        if (threadIdx.x < AME_TILE) {
+            aJ[buf][threadIdx.x] = sa;
+            bJ[buf][threadIdx.x] = sb;
+        }
+    };
+    auto stage = [&](int J, int buf) {
+        stage_load(J);
+        stage_store(buf);
     };
 
     double quad = 0.0, sq = 0.0;
@@ -136,37 +161,46 @@ ame_pairs_kernel(ame_dims dm, const float* __restrict__ Yt, const float* __restr
         __syncthreads();   // the previous strip's last tile is done with both buffers
         stage(Jb, 0);
         __syncthreads();
-        for (int J = Jb; J < nb; ++J) {
-            const int buf = (J - Jb) & 1;
-            if (J + 1 < nb) stage(J + 1, buf ^ 1);
+        // Y of half a tile (sub-tiles 2 hf, 2 hf + 1) of tile J: row i, columns
+        // J0 + 16 sub + {2 lq, 2 lq + 1} and {8 + 2 lq, 9 + 2 lq}; each 16-byte load of
+        // a wave covers 64 contiguous bytes of 16 rows (the A operand rows are
+        // permuted to match, below).  Half tiles rotate through two register
+        // buffers: the next half is always in flight behind the one being used.
+        auto load_half = [&](int J, int hf, float4 (&y)[2][2]) {
             const int J0 = J * AME_TILE;
-            // Y runs of the 4 sub-tiles: row i, columns J0 + 16 sub + 4 lq .. +3
-            float4 y[4][2];
 #pragma unroll
-            for (int sub = 0; sub < 4; ++sub) {
-                const int j0 = J0 + 16 * sub + 4 * lq;
-                if (irow && j0 + 4 <= n && (n & 1) == 0) {   // 16-byte aligned run inside the row
-                    const float4* yp = (const float4*)(ys + ((size_t)i * n + j0) * 2);
-                    y[sub][0] = yp[0];
-                    y[sub][1] = yp[1];
-                } else {                                      // row end / odd n: per element
-                    float t[8];
+            for (int s2 = 0; s2 < 2; ++s2) {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const bool ok = irow && j0 + e < n;
-                        const float2 v = ok ? *(const float2*)(ys + ((size_t)i * n + j0 + e) * 2)
-                                            : make_float2(0.f, 0.f);
-                        t[2 * e] = v.x;
-                        t[2 * e + 1] = v.y;
+                for (int h = 0; h < 2; ++h) {
+                    const int j0 = J0 + 16 * (2 * hf + s2) + 8 * h + 2 * lq;
+                    if (irow && j0 + 2 <= n && (n & 1) == 0) {
+                        // read once: non-temporal (MI355X_MICROARCH.md nt-weights)
+                        y[s2][h] = __builtin_nontemporal_load((const float4*)(ys + ((size_t)i * n + j0) * 2));
+                    } else {                                  // row end / odd n: per element
+                        float t[4];
+#pragma unroll
+                        for (int e = 0; e < 2; ++e) {
+                            const bool ok = irow && j0 + e < n;
+                            const float2 v = ok ? *(const float2*)(ys + ((size_t)i * n + j0 + e) * 2)
+                                                : make_float2(0.f, 0.f);
+                            t[2 * e] = v.x;
+                            t[2 * e + 1] = v.y;
+                        }
+                        y[s2][h] = make_float4(t[0], t[1], t[2], t[3]);
                     }
-                    y[sub][0] = make_float4(t[0], t[1], t[2], t[3]);
-                    y[sub][1] = make_float4(t[4], t[5], t[6], t[7]);
                 }
             }
+        };
+        float tq = 0.f, ts = 0.f;
+        auto half = [&](int J, int hf, int buf, const float4 (&y)[2][2]) {
+            const int J0 = J * AME_TILE;
 #pragma unroll
-            for (int sub = 0; sub < 4; ++sub) {
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const int sub = 2 * hf + s2;
                 f32x4 g1 = {0.f, 0.f, 0.f, 0.f}, g2 = {0.f, 0.f, 0.f, 0.f};
-                const int jr = 16 * sub + li;     // A operand row (column j of the tile)
+                // A operand row r = li holds column perm(r) = 2(r>>2) + (r&1) + 8((r>>1)&1),
+                // so accumulator v of lane (li, lq) is column 2 lq + (v&1) + 8 (v>>1)
+                const int jr = 16 * sub + 2 * (li >> 2) + (li & 1) + 8 * ((li >> 1) & 1);
 #pragma unroll
                 for (int kk = 0; kk < RP / 4; ++kk) {
                     const float av = VJ[buf][jr * LD + 4 * kk + lq];
@@ -174,11 +208,11 @@ ame_pairs_kernel(ame_dims dm, const float* __restrict__ Yt, const float* __restr
                     g1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bu[kk], g1, 0, 0, 0);
                     g2 = __builtin_amdgcn_mfma_f32_16x16x4f32(au, bv[kk], g2, 0, 0, 0);
                 }
-                const float yv[8] = {y[sub][0].x, y[sub][0].y, y[sub][0].z, y[sub][0].w,
-                                     y[sub][1].x, y[sub][1].y, y[sub][1].z, y[sub][1].w};
+                const float yv[8] = {y[s2][0].x, y[s2][0].y, y[s2][0].z, y[s2][0].w,
+                                     y[s2][1].x, y[s2][1].y, y[s2][1].z, y[s2][1].w};
 #pragma unroll
                 for (int v = 0; v < 4; ++v) {
-                    const int jl = 16 * sub + 4 * lq + v;
+                    const int jl = 16 * sub + 2 * lq + (v & 1) + 8 * (v >> 1);
                     const int j = J0 + jl;
                     if (!irow || j >= n || i == j) continue;
                     if (swap_mode && i > j) continue;
@@ -187,13 +221,27 @@ ame_pairs_kernel(ame_dims dm, const float* __restrict__ Yt, const float* __restr
                     const float e0 = yv[2 * v] - mu0, e1 = yv[2 * v + 1] - mu1;
                     const float se = e0 * e0 + e1 * e1;
                     if (i < j) {
-                        quad += (double)(e0 * (p * e0 + q01 * e1) + e1 * (q10 * e0 + sr * e1));
-                        sq += swap_mode ? 2.0 * (double)se : (double)se;
+                        tq += e0 * (p * e0 + q01 * e1) + e1 * (q10 * e0 + sr * e1);
+                        ts += swap_mode ? 2.f * se : se;
                     } else {
-                        sq += (double)se;
+                        ts += se;
                     }
                 }
             }
+        };
+        float4 y0[2][2], y1[2][2];
+        load_half(Jb, 0, y0);
+        for (int J = Jb; J < nb; ++J) {
+            const int buf = (J - Jb) & 1;
+            if (J + 1 < nb) stage_load(J + 1);
+            load_half(J, 1, y1);
+            half(J, 0, buf, y0);
+            if (J + 1 < nb) load_half(J + 1, 0, y0);
+            half(J, 1, buf, y1);
+            quad += (double)tq;      // this tile's sums (<= 16 terms per lane)
+            sq += (double)ts;
+            tq = ts = 0.f;
+            if (J + 1 < nb) stage_store(buf ^ 1);
             __syncthreads();
         }
     }
@@ -214,10 +262,20 @@ __global__ void __launch_bounds__(AME_NT)
 ame_nodes_kernel(ame_dims dm, const float* __restrict__ x, const float* __restrict__ prev_final,
                  const double* __restrict__ cov_terms, const double* __restrict__ consts,
                  const double* __restrict__ phi, double* __restrict__ partial) {
+    // One thread per (node, slice); the three d x d matrices it contracts with
+    // (Sigma0^-1, Q^-1, Phi) are staged in LDS once per workgroup, so every
+    // thread's matvecs read broadcast LDS words instead of global memory.
     constexpr int D = 2 + 2 * R;
+    constexpr int DD = D * D;
     const int n = dm.n;
-    const size_t DD = (size_t)D * D;
+    __shared__ double cS0[DD], cQ[DD], cPhi[DD];
     __shared__ double red[4 * 6];
+    for (int e = threadIdx.x; e < DD; e += AME_NT) {
+        cS0[e] = consts[e];
+        cQ[e] = consts[DD + e];
+        cPhi[e] = phi[e];
+    }
+    __syncthreads();
     const int idx = blockIdx.x * AME_NT + threadIdx.x;
     double v[6] = {0, 0, 0, 0, 0, 0};
     if (idx < dm.T_local * n) {
@@ -227,38 +285,37 @@ ame_nodes_kernel(ame_dims dm, const float* __restrict__ x, const float* __restri
         const double* ct = cov_terms + ((size_t)tl * n + i) * 4;
         v[4] = ct[0];
         v[5] = ct[1];
+        double e[D];
+        const double* M;
         if (tg == 0) {
-            double qsum = 0.0;
 #pragma unroll
-            for (int k = 0; k < D; ++k) {
-                double row = 0.0;
-#pragma unroll
-                for (int m = 0; m < D; ++m) row = fma(consts[(size_t)k * D + m], (double)mu[m], row);
-                qsum = fma((double)mu[k], row, qsum);
-            }
-            v[0] = qsum;
+            for (int k = 0; k < D; ++k) e[k] = (double)mu[k];
+            M = cS0;
             v[1] = ct[3];
         } else {
             const float* pr = (tl > 0) ? x + ((size_t)(tl - 1) * n + i) * D : prev_final + (size_t)i * D;
-            double e[D];
+            double pm[D];
+#pragma unroll
+            for (int m = 0; m < D; ++m) pm[m] = (double)pr[m];
 #pragma unroll
             for (int k = 0; k < D; ++k) {
-                double pm = 0.0;
+                double acc = 0.0;
 #pragma unroll
-                for (int m = 0; m < D; ++m) pm = fma(phi[(size_t)k * D + m], (double)pr[m], pm);
-                e[k] = (double)mu[k] - pm;
+                for (int m = 0; m < D; ++m) acc = fma(cPhi[k * D + m], pm[m], acc);
+                e[k] = (double)mu[k] - acc;
             }
-            double qsum = 0.0;
-#pragma unroll
-            for (int k = 0; k < D; ++k) {
-                double row = 0.0;
-#pragma unroll
-                for (int m = 0; m < D; ++m) row = fma(consts[DD + (size_t)k * D + m], e[m], row);
-                qsum = fma(e[k], row, qsum);
-            }
-            v[2] = qsum;
+            M = cQ;
             v[3] = ct[2];
         }
+        double qsum = 0.0;
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            double row = 0.0;
+#pragma unroll
+            for (int m = 0; m < D; ++m) row = fma(M[k * D + m], e[m], row);
+            qsum = fma(e[k], row, qsum);
+        }
+        v[(tg == 0) ? 0 : 2] = qsum;
     }
     block_sum<6>(v, red);
     if (threadIdx.x == 0)

@@ -1,0 +1,16 @@
+#!/bin/bash
+# ELBO parity subset + isolated ELBO-side kernel statistics (rocprofv3).
+set -o pipefail
+OUT=gpurun_out/${1:-elbo}; mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_baseline_shapes.py -m gpu -x -q --timeout 300 --timeout-method thread -k "golden or oracle or config3 or swap or config2" \
+   > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 $OUT/pytest_gpu.log; exit 1; }
+tail -1 $OUT/pytest_gpu.log
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- \
+    python3 -u tools/elbo_iso.py > $OUT/iso.txt 2> $OUT/iso.err || { echo "iso failed"; tail -20 $OUT/iso.err; exit 1; }
+cat $OUT/iso.txt
+F=$(find $OUT/stats -name '*kernel_stats.csv' | head -1); cp $F $OUT/kernel_stats.csv
+python3 -c "
+import csv
+for r in csv.DictReader(open('$OUT/kernel_stats.csv')):
+    if 'ame_' in r['Name']: print(r['Name'][:50], r['Calls'], round(float(r['AverageNs'])/1e3,1), 'us', 'min', round(float(r['MinNs'])/1e3,1))"
