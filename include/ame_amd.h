@@ -75,7 +75,7 @@ typedef struct ame_sweep_args {
     uint64_t* hand;              /* [T_local][n][d] {epoch,value} granules, lane hand-off */
     const uint64_t* halo_in;     /* [n][d] granules of slice t_begin-1 (left rank), or NULL */
     uint64_t* halo_out;          /* [n][d] granules of slice t_begin+T_local-1 for the right
-                                    rank (peer/host-mapped), or NULL */
+                                    rank (its peer buffer, ame_peer_open), or NULL */
     float* cov;                  /* [T_local][n][d][d] covariances before the sweep (damped in
                                     place when cov_new is NULL) */
     const double* consts;        /* fp64 [5][d][d] */
@@ -97,9 +97,9 @@ typedef struct ame_sweep_args {
                                     epoch, so the next sweep can be queued while the previous one
                                     (epoch wait_epoch) still runs.  Needs ame_sweep_orders_slices()
                                     and room for both sweeps' workgroups (2 T_local <= max_slices) */
-    float* back_out;             /* time-sharded, rank with a left neighbour: host-mapped
-                                    [n*d floats | done word at AME_BACK_DONE_OFFSET] the first slice
-                                    fills with its new means when it finishes, or NULL */
+    float* back_out;             /* time-sharded, rank with a left neighbour: that rank's peer
+                                    buffer [n*d floats | done word at AME_BACK_DONE_OFFSET] the first
+                                    slice fills with its new means when it finishes, or NULL */
     const float* back_in;        /* the right neighbour's back_out: in a pipelined launch
                                     (wait_epoch != 0) it replaces next_old */
 } ame_sweep_args;
@@ -164,11 +164,23 @@ int ame_elbo(const ame_dims* dims, const ame_elbo_args* args, void* stream);
 /* Scratch doubles ame_elbo needs. */
 long long ame_elbo_work_size(const ame_dims* dims);
 
-/* Pin + map host memory (e.g. a shared-memory halo buffer mapped by two
- * processes) for device access; *dev receives the device address.  Used by the
- * time-sharded multi-GPU path for the boundary-mean granule hand-off. */
+/* Pin + map host memory for device access; *dev receives the device address
+ * (utility; the multi-GPU path uses the peer buffers below). */
 int ame_host_register(void* host, unsigned long long bytes, void** dev);
 int ame_host_unregister(void* host);
+
+/* Peer hand-off buffers of the time-sharded multi-GPU path (one process per
+ * GPU, all on one node, xGMI).  ame_peer_alloc: zeroed fine-grained device
+ * memory on the current device plus its IPC handle (AME_PEER_HANDLE_BYTES
+ * bytes written to *handle); a neighbour process maps it with ame_peer_open and
+ * writes boundary means into it with system-scope stores while the owner's
+ * sweep polls it locally.  No host memory is involved.  Replaces nothing in the
+ * reference (single process, structured_mf.py:240 loops over all T). */
+#define AME_PEER_HANDLE_BYTES 64
+int ame_peer_alloc(unsigned long long bytes, void** dev, void* handle);
+int ame_peer_free(void* dev);
+int ame_peer_open(const void* handle, void** dev);
+int ame_peer_close(void* dev);
 
 /* ---- post-fit alignment -------------------------------
  * Replaces the per-time-step loops of src/utils/alignment.py:

@@ -16,6 +16,7 @@ AME_GOOD, AME_BAD, AME_NAIVE = 0, 1, 2
 AME_STATUS_SPIN_TIMEOUT = 1
 AME_STATUS_HALO_TIMEOUT = 2
 AME_STATUS_LDS_TIMEOUT = 4
+AME_PEER_HANDLE_BYTES = 64
 
 c_int32 = ctypes.c_int32
 c_vp = ctypes.c_void_p
@@ -48,6 +49,7 @@ class ame_elbo_args(ctypes.Structure):
 # every symbol include/ame_amd.h declares (checked by tests/test_capi.py)
 EXPORTS = ("ame_pack_y", "ame_sweep", "ame_sweep_work_size", "ame_sweep_orders_slices", "ame_sweep_max_slices", "ame_sweep_lds_bytes", "ame_cov",
            "ame_elbo", "ame_elbo_work_size", "ame_host_register", "ame_host_unregister",
+           "ame_peer_alloc", "ame_peer_free", "ame_peer_open", "ame_peer_close",
            "ame_supported_r", "ame_last_error", "ame_version", "ame_align_work_size",
            "ame_align_cross_size", "ame_align_partials_size", "ame_align_cross", "ame_align_apply")
 
@@ -75,6 +77,10 @@ def _declare(L):
     L.ame_supported_r.argtypes = [P(ctypes.c_int), ctypes.c_int]
     L.ame_host_register.argtypes = [c_vp, ctypes.c_ulonglong, P(c_vp)]
     L.ame_host_unregister.argtypes = [c_vp]
+    L.ame_peer_alloc.argtypes = [ctypes.c_ulonglong, P(c_vp), c_vp]
+    L.ame_peer_free.argtypes = [c_vp]
+    L.ame_peer_open.argtypes = [c_vp, P(c_vp)]
+    L.ame_peer_close.argtypes = [c_vp]
     ci = ctypes.c_int
     for name in ("ame_align_work_size", "ame_align_cross_size"):
         getattr(L, name).restype = ctypes.c_longlong
@@ -89,7 +95,8 @@ def _declare(L):
     L.ame_last_error.restype = ctypes.c_char_p
     L.ame_version.restype = ctypes.c_char_p
     for name in ("ame_pack_y", "ame_sweep", "ame_cov", "ame_elbo", "ame_sweep_max_slices",
-                 "ame_supported_r", "ame_host_register", "ame_host_unregister"):
+                 "ame_supported_r", "ame_host_register", "ame_host_unregister", "ame_peer_alloc",
+                 "ame_peer_free", "ame_peer_open", "ame_peer_close"):
         getattr(L, name).restype = ctypes.c_int
     return L
 

@@ -119,6 +119,41 @@ int ame_host_unregister(void* host) {
     return hipHostUnregister(host) == hipSuccess ? 0 : fail("ame_host_unregister failed");
 }
 
+int ame_peer_alloc(unsigned long long bytes, void** dev, void* handle) {
+    if (!dev || !handle || bytes == 0) return fail("ame_peer_alloc: bad arguments");
+    hipError_t e = hipExtMallocWithFlags(dev, (size_t)bytes, hipDeviceMallocFinegrained);
+    if (e == hipSuccess) e = hipMemset(*dev, 0, (size_t)bytes);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipIpcGetMemHandle((hipIpcMemHandle_t*)handle, *dev);
+    if (e != hipSuccess) {
+        snprintf(g_err, sizeof(g_err), "ame_peer_alloc: %s", hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+}
+
+int ame_peer_free(void* dev) {
+    if (!dev) return fail("ame_peer_free: NULL");
+    return hipFree(dev) == hipSuccess ? 0 : fail("ame_peer_free failed");
+}
+
+int ame_peer_open(const void* handle, void** dev) {
+    if (!handle || !dev) return fail("ame_peer_open: bad arguments");
+    hipIpcMemHandle_t h;
+    memcpy(&h, handle, sizeof(h));
+    hipError_t e = hipIpcOpenMemHandle(dev, h, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) {
+        snprintf(g_err, sizeof(g_err), "ame_peer_open: hipIpcOpenMemHandle: %s", hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+}
+
+int ame_peer_close(void* dev) {
+    if (!dev) return fail("ame_peer_close: NULL");
+    return hipIpcCloseMemHandle(dev) == hipSuccess ? 0 : fail("ame_peer_close failed");
+}
+
 long long ame_sweep_lds_bytes(int n, int r) {
     if (!r_supported(r) || n < 1) return 0;
     return sweep_lds_layout(n, r, ame_sweep_force_global()).total;

@@ -174,8 +174,9 @@ ame_pairs_kernel(ame_dims dm, const float* __restrict__ Yt, const float* __restr
                 for (int h = 0; h < 2; ++h) {
                     const int j0 = J0 + 16 * (2 * hf + s2) + 8 * h + 2 * lq;
                     if (irow && j0 + 2 <= n && (n & 1) == 0) {
-                        // read once: non-temporal (MI355X_MICROARCH.md nt-weights)
-                        y[s2][h] = __builtin_nontemporal_load((const float4*)(ys + ((size_t)i * n + j0) * 2));
+                        // default cache policy: non-temporal loads measured slower here
+                        // (166 vs 155 us at config 3)
+                        y[s2][h] = *(const float4*)(ys + ((size_t)i * n + j0) * 2);
                     } else {                                  // row end / odd n: per element
                         float t[4];
 #pragma unroll

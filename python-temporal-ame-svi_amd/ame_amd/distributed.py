@@ -10,28 +10,32 @@ terms of the boundary slices (structured_mf.py:255-264):
   sweep;
 * left halo, NEW means of slice t_begin-1 (last slice of rank g-1) -- produced
   node by node DURING the same sweep (exact Gauss-Seidel order): rank g-1's last
-  sweep lane writes {epoch,value} granules into a host-shared buffer that both
-  processes map (hipHostRegister), and rank g's first lane polls them.  No
-  collective sits on the data path; the wavefront simply continues across the
-  GPU boundary;
+  sweep lane stores {epoch,value} granules with system-scope stores straight
+  into a buffer in rank g's HBM (xGMI peer write), and rank g's first lane polls
+  its local copy.  No collective and no host memory sit on the data path; the
+  wavefront simply continues across the GPU boundary;
 * after the sweep: all_gather of last-slice means (the transition term of the
   ELBO at t_begin) and an fp64 all_reduce of the 8 ELBO/MSE sums;
 * pipelined sweeps (the next sweep queued while this one runs): the right halo
   cannot come from a collective, so each rank's first slice also writes its
-  final means into a back channel in the same shared buffer when it finishes
-  (system-scope release + done word), and the left rank's last slice of the
-  next sweep waits for that word instead.
+  final means into a back channel in rank g-1's HBM when it finishes
+  (system-scope release + done word), and rank g-1's last slice of the next
+  sweep waits for that word instead.
+
+Every peer buffer lives on the GPU that POLLS it (fine-grained device memory,
+exported with an IPC handle, ame_peer_alloc / ame_peer_open); the neighbour
+only writes into it.  The handles travel over the process group.  All ranks
+must be on one node (xGMI); that is checked at setup.
 
 ``shard_range`` / ``assemble``-level logic is exercised on CPU by
-tests/test_distributed_cpu.py (gloo, world_size 2).
+tests/test_distributed_cpu.py (gloo, world_size 2); the peer buffers by
+tests/test_gpu_distributed.py (2-4 processes on one GPU: same-device IPC).
 """
 from __future__ import annotations
 
 import atexit
 import ctypes
-import mmap
-import os
-import uuid
+import socket
 from typing import Optional, Tuple
 
 import torch
@@ -52,48 +56,33 @@ def shard_range(T: int, world: int, rank: int) -> Tuple[int, int]:
     return t_begin, base + (1 if rank < extra else 0)
 
 
-class HostHalo:
-    """A granule buffer in /dev/shm, pinned and mapped for device access."""
+class PeerBuffer:
+    """Fine-grained device memory: owned (allocated here, exported) or mapped
+    (opened from a neighbour's handle)."""
 
-    def __init__(self, path: str, nbytes: int, create: bool):
-        self.path, self.nbytes = path, nbytes
-        flags = os.O_RDWR | (os.O_CREAT | os.O_EXCL if create else 0)
-        fd = os.open(path, flags, 0o600)
-        try:
-            if create:
-                os.ftruncate(fd, nbytes)
-            self.mm = mmap.mmap(fd, nbytes, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
-        finally:
-            os.close(fd)
-        if create:
-            self.mm[:] = bytes(nbytes)
-        self._cbuf = (ctypes.c_char * nbytes).from_buffer(self.mm)
-        self.host = ctypes.c_void_p(ctypes.addressof(self._cbuf))
-        dev = ctypes.c_void_p()
-        _lib.check(_lib.lib().ame_host_register(self.host, nbytes, ctypes.byref(dev)),
-                   "ame_host_register")
-        self.dev = dev
-        self.owner = create
+    def __init__(self, nbytes: int = 0, handle: Optional[bytes] = None):
+        L = _lib.lib()
+        self.dev = ctypes.c_void_p()
+        if handle is None:
+            h = (ctypes.c_char * _lib.AME_PEER_HANDLE_BYTES)()
+            _lib.check(L.ame_peer_alloc(nbytes, ctypes.byref(self.dev), h), "ame_peer_alloc")
+            self.handle = bytes(h)
+            self.owner = True
+        else:
+            h = (ctypes.c_char * _lib.AME_PEER_HANDLE_BYTES).from_buffer_copy(handle)
+            _lib.check(L.ame_peer_open(h, ctypes.byref(self.dev)), "ame_peer_open")
+            self.handle = handle
+            self.owner = False
 
     def close(self):
-        if self.mm is None:
+        if self.dev is None or not self.dev.value:
             return
         try:
-            _lib.lib().ame_host_unregister(self.host)
+            L = _lib.lib()
+            (L.ame_peer_free if self.owner else L.ame_peer_close)(self.dev)
         except Exception:
             pass
-        self.host = None
-        self._cbuf = None
-        try:
-            self.mm.close()
-        except BufferError:
-            pass
-        self.mm = None
-        if self.owner:
-            try:
-                os.unlink(self.path)
-            except FileNotFoundError:
-                pass
+        self.dev = None
 
 
 class TimeShardHalo:
@@ -102,8 +91,7 @@ class TimeShardHalo:
     def __init__(self, shard: Shard, group=None):
         self.shard = shard
         self.group = group
-        self.left: Optional[HostHalo] = None
-        self.right: Optional[HostHalo] = None
+        self._peers = None       # (own halo, own back, peer halo, peer back) PeerBuffers
         self._next_old = None
         self._prev_final = None
         # gloo (CPU tests, several ranks sharing one GPU) needs host staging
@@ -121,28 +109,38 @@ class TimeShardHalo:
 
     # ---- setup (called once the engine knows n, d) ----
     def _setup(self, eng):
-        if self.left is not None or self.right is not None or self.shard.world == 1:
+        if self._peers is not None or self.shard.world == 1:
             return
-        tag = [uuid.uuid4().hex[:12] if self.shard.rank == 0 else None]
-        dist.broadcast_object_list(tag, src=0, group=self.group)
-        nd = eng.n * eng.d
-        self._back_off = nd * 8                                    # after the granules
-        nbytes = max(4096, self._back_off + (((nd + 63) // 64) * 64 + 64) * 4)
         rank, world = self.shard.rank, self.shard.world
-        base = f"/dev/shm/ame_halo_{tag[0]}"
-        if rank > 0:   # consumer of boundary (rank-1 -> rank) creates it
-            self.left = HostHalo(f"{base}_{rank - 1}", nbytes, create=True)
-        dist.barrier(group=self.group)
-        if rank < world - 1:
-            self.right = HostHalo(f"{base}_{rank}", nbytes, create=False)
+        hosts = [None] * world
+        dist.all_gather_object(hosts, socket.gethostname(), group=self.group)
+        if len(set(hosts)) != 1:
+            raise RuntimeError(
+                "ame_amd: time-sharded ranks hand boundary means over xGMI peer memory and "
+                f"must all run on one node; got hosts {sorted(set(hosts))}")
+        nd = eng.n * eng.d
+        self._back_bytes = (((nd + 63) // 64) * 64 + 64) * 4      # floats + done word
+        with torch.cuda.device(eng.dev):
+            # buffers this rank POLLS: its left halo (granules from rank-1) and the
+            # back channel of its right boundary (final means of rank+1's first slice)
+            own_halo = PeerBuffer(nd * 8) if rank > 0 else None
+            own_back = PeerBuffer(self._back_bytes) if rank < world - 1 else None
+            mine = (own_halo.handle if own_halo else None, own_back.handle if own_back else None)
+            allh = [None] * world
+            dist.all_gather_object(allh, mine, group=self.group)
+            peer_halo = PeerBuffer(handle=allh[rank + 1][0]) if rank < world - 1 else None
+            peer_back = PeerBuffer(handle=allh[rank - 1][1]) if rank > 0 else None
+        self._peers = (own_halo, own_back, peer_halo, peer_back)
         dist.barrier(group=self.group)
         atexit.register(self.close)
 
     def close(self):
-        for h in (self.left, self.right):
-            if h is not None:
-                h.close()
-        self.left = self.right = None
+        if self._peers is None:
+            return
+        for p in self._peers:
+            if p is not None:
+                p.close()
+        self._peers = None
 
     def _all_gather_slice(self, t: torch.Tensor):
         src = self._coll(t.contiguous())
@@ -160,14 +158,13 @@ class TimeShardHalo:
 
     def back_channels(self, eng):
         """(back_in, back_out) device addresses: the right boundary's back channel
-        is read by this rank's last slice, the left one written by its first."""
+        (local) is read by this rank's last slice; the left one (rank-1's HBM) is
+        written by its first."""
         self._setup(eng)
-        back_in = back_out = None
-        if self.right is not None:
-            back_in = ctypes.c_void_p(self.right.dev.value + self._back_off)
-        if self.left is not None:
-            back_out = ctypes.c_void_p(self.left.dev.value + self._back_off)
-        return back_in, back_out
+        if self._peers is None:
+            return None, None
+        own_halo, own_back, peer_halo, peer_back = self._peers
+        return (own_back.dev if own_back else None), (peer_back.dev if peer_back else None)
 
     def before_sweep(self, eng, gather=True, first=None):
         """first: this rank's first slice of the sweep's input state (the
@@ -180,8 +177,11 @@ class TimeShardHalo:
             if rank < world - 1:
                 self._next_old = firsts[rank + 1]
                 next_old = ctypes.c_void_p(self._next_old.data_ptr())
-        halo_in = self.left.dev if self.left is not None else None
-        halo_out = self.right.dev if self.right is not None else None
+        halo_in = halo_out = None
+        if self._peers is not None:
+            own_halo, _, peer_halo, _ = self._peers
+            halo_in = own_halo.dev if own_halo else None
+            halo_out = peer_halo.dev if peer_halo else None
         return next_old, halo_in, halo_out
 
     def after_sweep(self, eng):
