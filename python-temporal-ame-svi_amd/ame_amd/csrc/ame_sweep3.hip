@@ -106,8 +106,6 @@ struct Cfg {
     static constexpr int LTQ = (NLT + NHB - 1) / NHB;
     static constexpr int NP = (4 * D <= 192) ? 4 : 2;       // AR row parts (HF1)
     static constexpr int MC = (D + NP - 1) / NP;
-    static constexpr int NHALF = (6 * D <= 256) ? 2 : 1;    // HF2 row halves
-    static constexpr int HD = D / NHALF;
     static constexpr int NC = (DD * 4 + 1023) / 1024;       // DMA KiB per covariance
 };
 
@@ -158,7 +156,7 @@ __global__ void __launch_bounds__(kNT)
 ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     using C = Cfg<R>;
     constexpr int D = C::D, M2 = C::M2, DD = C::DD, NSREG = C::NSREG, MP = C::MP;
-    constexpr int NLT = C::NLT, LTQ = C::LTQ, NP = C::NP, MC = C::MC, NHALF = C::NHALF, HD = C::HD;
+    constexpr int NLT = C::NLT, LTQ = C::LTQ, NP = C::NP, MC = C::MC;
     constexpr int NC = C::NC;
     const int n = dm.n, TL = dm.T_local, Tt = dm.T_total;
     const int b = blockIdx.x;
@@ -184,7 +182,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     float* mu32 = (float*)(smem + LY::oMu32);
     double* g64 = (double*)(smem + LY::oG);
     double* jn64 = (double*)(smem + LY::oJn);
-    double* vbuf = (double*)(smem + LY::oV);
+    double* vbuf = (double*)(smem + LY::oV);          // prologue pivot scratch
     double* dots = (double*)(smem + LY::oDots);
     double* red = (double*)(smem + LY::oRed);
     float* gp = (float*)(smem + LY::oGP);
@@ -591,26 +589,6 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         }
         if (k < D && p == 0) g64[(m & 1) * D + k] = g;
     };
-    // HF2 (hw 3..6): v = K g, yv = K Jn^T for node m with base Kb
-    auto hf2 = [&](int m, const double* Kb) {
-        const int q = tid - 256;
-        const int k = q / (3 * NHALF), rem = q - k * (3 * NHALF);
-        const int vsel = rem / NHALF, half = rem - vsel * NHALF;
-        const int kc = (k < D) ? k : 0;
-        const double* vec = (vsel == 0) ? g64 + (m & 1) * D : jn64 + (vsel - 1) * D;
-        const double* kr = Kb + (size_t)kc * D;
-        const int c0 = half * HD;
-        double acc = 0.0;
-#pragma unroll
-        for (int c = 0; c < HD; ++c) acc = fma(kr[c0 + c], vec[c0 + c], acc);
-        const double accA = kr[0] * vec[0] + kr[1] * vec[1];
-        if constexpr (NHALF == 2) acc = dpp_add_xor1(acc);
-        if (k < D && half == 0) {
-            double* vo = vbuf + ((m & 1) * D + k) * 4;
-            vo[vsel] = acc;
-            if (vsel == 0) vo[3] = accA;
-        }
-    };
     auto jn_fill = [&](int node) {   // J rows of `node` (old) -> jn64; lanes < D of the calling wave
         if (lane < D) {
             double j0, j1;
@@ -649,7 +627,6 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     __syncthreads();
     if (wave >= 1 && hw <= 2) hf1(0);
     __syncthreads();
-    if (wave >= 4) hf2(0, Kbuf);
     if (wave == 7) {   // Y rows 2..4 (slots 2,3,0), covariances of nodes 0,1, granules of nodes 1..3
         for (int q = 2; q <= 4; ++q) dma_y(q);
         for (int q = 0; q <= 1; ++q) dma_cov(q);
@@ -669,6 +646,31 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         double brow[D];   // row k of the base inverse B_i
 #pragma unroll
         for (int c = 0; c < D; ++c) brow[c] = kl ? Kbuf[(size_t)k * D + c] : 0.0;
+        // v = B g, yv = B Jn^T (Jn: J rows of node i+1, old) and this lane's Jn
+        // entries, for the coming step; B = brow, g and Jn from HF1 / jn_fill.
+        // Runs at the end of the previous step, after the solver's own work.
+        double v = 0, yv0 = 0, yv1 = 0, vA = 0, nq0 = 0, nq1 = 0;
+        auto prep = [&](int node) {
+            if (!kl) return;
+            const double* gg = g64 + (node & 1) * D;
+            double s0 = 0, s1 = 0, s2 = 0, t0 = 0, t1 = 0, t2 = 0;
+#pragma unroll
+            for (int c = 0; c < D; c += 2) {
+                s0 = fma(brow[c], gg[c], s0);
+                s1 = fma(brow[c], jn64[c], s1);
+                s2 = fma(brow[c], jn64[D + c], s2);
+                t0 = fma(brow[c + 1], gg[c + 1], t0);
+                t1 = fma(brow[c + 1], jn64[c + 1], t1);
+                t2 = fma(brow[c + 1], jn64[D + c + 1], t2);
+            }
+            v = s0 + t0;
+            yv0 = s1 + t1;
+            yv1 = s2 + t2;
+            vA = brow[0] * gg[0] + brow[1] * gg[1];
+            nq0 = jn64[k];
+            nq1 = jn64[D + k];
+        };
+        prep(0);
         double Wp0 = 0, Wp1 = 0, Xp0 = 0, Xp1 = 0, Lp0 = 0, Lp1 = 0, Gp0 = 0, Gp1 = 0;
         Mat2 Mip = m2(0, 0, 0, 0), Sip = m2(0, 0, 0, 0);
         for (int i = 0; i < n; ++i) {
@@ -679,8 +681,6 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             const float* mup = mu32 + ppar * D;       // mu_{i-1} (fp32)
             const double* mupd = mu64 + ppar * D;     // mu_{i-1} (fp64)
             const double msk = kl ? 1.0 : 0.0;
-            const double* vi = vbuf + (par * D + kc) * 4;
-            const double v = msk * vi[0], yv0 = msk * vi[1], yv1 = msk * vi[2], vA = msk * vi[3];
             const double g = msk * g64[par * D + kc];
             double J0, J1;
             jcol<R>(mup, has_prev && kl, kc, J0, J1);
@@ -701,8 +701,8 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 kj1 = s1a + s1b;
             }
             STAMP3(1);
-            // critical reduction: a1(4) a2(4) c(4) e(2) jy(4) eA(2)
-            constexpr int NV = 20;
+            // critical reduction: a1(4) a2(4) c(4) e(2) jy(4) eA(2) ny(4)
+            constexpr int NV = 24;
             double pr[NV];
             pr[0] = Wp0 * J0; pr[1] = Wp0 * J1; pr[2] = Wp1 * J0; pr[3] = Wp1 * J1;       // a1[p][q]
             pr[4] = Xp0 * J0; pr[5] = Xp0 * J1; pr[6] = Xp1 * J0; pr[7] = Xp1 * J1;       // a2[p][q]
@@ -710,6 +710,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             pr[12] = J0 * v; pr[13] = J1 * v;                                             // e[q]
             pr[14] = J0 * yv0; pr[15] = J0 * yv1; pr[16] = J1 * yv0; pr[17] = J1 * yv1;   // jy[q][p]
             pr[18] = J0 * vA; pr[19] = J1 * vA;                                           // eA[q]
+            pr[20] = nq0 * yv0; pr[21] = nq0 * yv1; pr[22] = nq1 * yv0; pr[23] = nq1 * yv1;   // ny[q][p]
             {
                 int idx;
                 const double sv = wave_reduce_scatter<NV>(pr, lane, idx);
@@ -725,15 +726,15 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             const V2 e = {o[12], o[13]};
             const Mat2 jy = m2(o[14], o[15], o[16], o[17]);
             const V2 eA = {o[18], o[19]};
+            const Mat2 ny = m2(o[20], o[21], o[22], o[23]);
             STAMP3(2);
-            // off-critical dots from helper wave hw 3
+            // off-critical dots from helper wave hw 5
             lds_wait_ge(ddone, (uint32_t)(i + 1), a.status, dead);
             STAMP3(3);
             const V2 b1 = {dots[0], dots[1]}, b2 = {dots[2], dots[3]};
             const Mat2 f1 = m2(dots[4], dots[5], dots[6], dots[7]);
             const Mat2 f2 = m2(dots[8], dots[9], dots[10], dots[11]);
-            const Mat2 ny = m2(dots[12], dots[13], dots[14], dots[15]);
-            const V2 b1A = {dots[16], dots[17]}, b2A = {dots[18], dots[19]};
+            const V2 b1A = {dots[12], dots[13]}, b2A = {dots[14], dots[15]};
             // raw y_{i,i-1}
             double y0 = 0, y1 = 0;
             if (has_prev) { y0 = (double)yst[(i & 3) * 4 + 0]; y1 = (double)yst[(i & 3) * 4 + 1]; }
@@ -832,6 +833,14 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 for (int c = 0; c < D; ++c) brow[c] = Kn[(size_t)k * D + c];
             }
             STAMP3(7);
+            if (i + 1 < n) {   // g_{i+1} and Jn of node i+2 from HF1 (hw 0..2)
+                lds_wait_ge(gcnt, 3u * (uint32_t)(i + 1), a.status, dead);
+                STAMP3(8);
+#ifndef AME_ABL_NOPREP
+                prep(i + 1);
+#endif
+                STAMP3(9);
+            }
             lds_barrier3();
         }
         {
@@ -863,20 +872,17 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 const double* rc = rec + (ppar * D + kc) * 8;
                 const double W0 = msk * rc[2], W1 = msk * rc[3], X0 = msk * rc[6], X1 = msk * rc[7];
                 const double g = g64[par * D + kc];
-                const double yv0 = vbuf[(par * D + kc) * 4 + 1], yv1 = vbuf[(par * D + kc) * 4 + 2];
                 double n0, n1;
                 jcol<R>(xring + ((i + 1) & 7) * 64, i + 1 < n, kc, n0, n1);
                 const double gA = (k < 2) ? g : 0.0;
-                double pr[20];
+                double pr[16];
                 pr[0] = W0 * g; pr[1] = W1 * g; pr[2] = X0 * g; pr[3] = X1 * g;           // b1, b2
                 pr[4] = W0 * n0; pr[5] = W0 * n1; pr[6] = W1 * n0; pr[7] = W1 * n1;       // f1[p][q]
                 pr[8] = X0 * n0; pr[9] = X0 * n1; pr[10] = X1 * n0; pr[11] = X1 * n1;     // f2[p][q]
-                pr[12] = msk * n0 * yv0; pr[13] = msk * n0 * yv1;                          // ny[q][p]
-                pr[14] = msk * n1 * yv0; pr[15] = msk * n1 * yv1;
-                pr[16] = W0 * gA; pr[17] = W1 * gA; pr[18] = X0 * gA; pr[19] = X1 * gA;   // b1A, b2A
+                pr[12] = W0 * gA; pr[13] = W1 * gA; pr[14] = X0 * gA; pr[15] = X1 * gA;   // b1A, b2A
                 int idx;
-                const double sv = wave_reduce_scatter<20>(pr, lane, idx);
-                if (idx < 20) dots[idx] = sv;
+                const double sv = wave_reduce_scatter<16>(pr, lane, idx);
+                if (idx < 16) dots[idx] = sv;
                 if (lane == 0) lds_signal_set(ddone, (uint32_t)(i + 1));
                 STAMP3(1);
             }
@@ -910,10 +916,14 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                         Kn[k * D + m] = kn;
                         Kn[m * D + k] = kn;
                     }
+#ifndef AME_ABL_NOCOVST
                     if (ok && i >= 1) {
                         cv[k * D + m] = n_km;
+#ifndef AME_ABL_NOTSTORE
                         if (k != m) cv[m * D + k] = n_mk;
+#endif
                     }
+#endif
                 }
             }
             STAMP3(4);
@@ -927,7 +937,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 wave_lds_sync3();
                 hf1(i + 1);
                 STAMP3(3);
-                if (hw == 0) jn_fill(i + 2);   // J rows of node i+2 for HF2
+                if (hw == 0) jn_fill(i + 2);   // J rows of node i+2 for the solver
                 if (lane == 0) lds_signal_add(gcnt, 1u);
             }
             if (i < n) {
@@ -953,7 +963,11 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                     }
                 }
                 // HE: GEMV of node i+2 (its Y row landed in the ring by step i-1)
+#ifdef AME_ABL_NOGEMV012
+                if (i + 2 < n && hw >= 3) gemv(i + 2, yring + (size_t)((i + 2) & 3) * YS);
+#else
                 if (i + 2 < n) gemv(i + 2, yring + (size_t)((i + 2) & 3) * YS);
+#endif
                 STAMP3(5);
                 // loader: this step's batch -- Y row i+5, covariance of node i+2, old
                 // means of node i+5 (slice t) and i+4 (slice t+1), granules of node i+4
@@ -964,14 +978,6 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                     dma_r(i + 4);
                     dma_p(i + 4);
                     STAMP3(6);
-                }
-                // HF2 (hw 3..6): v_{i+1}, yv_{i+1} with K_i
-                if (hw >= 3 && i + 1 < n) {
-                    lds_wait_ge(kcnt, 7u * (uint32_t)(i + 1), a.status, dead);
-                    lds_wait_ge(gcnt, 3u * (uint32_t)(i + 1), a.status, dead);
-                    STAMP3(7);
-                    hf2(i + 1, Kn);
-                    STAMP3(8);
                 }
             }
             // the batch issued 2 steps ago must have landed before the next step reads it

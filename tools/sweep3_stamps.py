@@ -20,10 +20,10 @@ SO = os.path.join(BDIR, f"libame_amd_stamps3{TAG}.so")
 SRCS = ("ame_sweep.hip", "ame_sweep3.hip", "ame_sweep4.hip", "ame_cov.hip", "ame_elbo.hip", "ame_capi.hip",
         "ame_selftest.hip", "ame_align.hip")
 NAMES = {
-    0: ["start", "J+kj", "reduce", "ddone", "2x2+assembly", "publish", "kcnt", "brow"],
+    0: ["start", "J+kj", "reduce", "ddone", "2x2+assembly", "publish", "kcnt", "brow", "gcnt", "prep(v,yv)"],
     1: ["start", "-", "poll", "hf1", "HB", "GEMV", "-", "-", "-", "end"],
-    2: ["start", "HX", "-", "-", "HB", "GEMV", "-", "kcnt", "hf2", "end"],
-    3: ["start", "-", "-", "-", "(no HB)", "GEMV", "DMA", "kcnt", "hf2", "vmwait"],
+    2: ["start", "HX", "-", "-", "HB", "GEMV", "-", "-", "-", "end"],
+    3: ["start", "-", "-", "-", "(no HB)", "GEMV", "DMA", "-", "-", "vmwait"],
 }
 WAVES = ["solver(w0)", "hw0(w1)", "hw5(w6)", "hw6(w7)"]
 
