@@ -140,7 +140,8 @@ struct Lay {
     static constexpr int oXr = al16(oCr + 4 * 4 * cs);             // [node&7] old means slice t, DMA
     static constexpr int oRr = al16(oXr + 8 * 256);                // [node&3] old means slice t+1, DMA
     static constexpr int oPr = al16(oRr + 4 * 256);                // [node&3] hand-off granules, DMA
-    static constexpr int oYr = al16(oPr + 4 * 1024);               // [node&3] Y rows (raw), DMA
+    static constexpr int oCs = al16(oPr + 4 * 1024);               // [node&1] new covariance, staged
+    static constexpr int oYr = al16(oCs + 4 * 2 * cs);             // [node&3] Y rows (raw), DMA
     __host__ __device__ static int ys(int n) { return ((n * 8 + 1023) / 1024) * 128; }   // float2
     __host__ __device__ static int oML(int n) { return al16(oYr + 4 * 8 * ys(n)); }
     __host__ __device__ static int total(int n, int nsreg) {
@@ -168,7 +169,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     const bool is_naive = dm.variant == AME_NAIVE, is_bad = dm.variant == AME_BAD;
     const int ns = (n + kNH - 1) / kNH;
     const int NY = (n * 8 + 1023) / 1024;     // DMA KiB per Y row
-    const int KDMA = NY + NC + 3;             // DMA instructions per step (loader wave)
+    const int KDMA = NY + NC + 2;             // DMA instructions per step (loader wave)
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     using LY = Lay<R>;
@@ -199,6 +200,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     float* xring = (float*)(smem + LY::oXr);
     float* rring = (float*)(smem + LY::oRr);
     uint64_t* pring = (uint64_t*)(smem + LY::oPr);
+    float* cst = (float*)(smem + LY::oCs);
     float2* mlds = (float2*)(smem + LY::oML(n));
 
     const double r00 = a.rinv[0], r01 = a.rinv[1], r10 = a.rinv[2], r11 = a.rinv[3];
@@ -290,6 +292,17 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         if (tg == 0 || node >= n) dma16(xo, dst);
         else if (tl == 0) dma16_sys(gran_src(node) + g2, dst);
         else dma16_sc1(gran_src(node) + g2, dst);
+    };
+
+    // staged new covariance of `node` -> cvw, 16 B per lane, whole rows (DD % 4 == 0)
+    auto flush_cov = [&](int node) {
+        const float4* src = (const float4*)(cst + (size_t)((node + 1) & 1) * LY::cs);
+        float4* dst = (float4*)(cvw + (size_t)node * DD);
+#pragma unroll
+        for (int q = 0; q < NC; ++q) {
+            const int e = q * 64 + lane;
+            if (e * 4 < DD) dst[e] = src[e];
+        }
     };
 
 #ifdef AME_STAMPS
@@ -864,6 +877,12 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             const int par = i & 1, ppar = (i + 1) & 1;
             const double* Bi = Kbuf + (size_t)par * DD;      // B_i
             double* Kn = Kbuf + (size_t)ppar * DD;           // K_i = B_{i+1}
+            // new covariance of node i-2 (staged by HB last step): coalesced stores
+            // (hw 4: no loads of its own to wait for)
+            if (hw == 4 && i >= 2) flush_cov(i - 2);
+            // granules of mu_{i+2,t-1} for HF1 at step i+1: one step ahead only, so
+            // they are current when they land (slice t trails slice t-1 by ~2 steps)
+            if (hw == 5 && i < n) dma_p(i + 2);
             // HX (hw 5, off the solver's SIMD): dots that do not involve mu_{i-1}
             if (hw == 5 && i < n) {
                 const int k = lane;
@@ -891,7 +910,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 const double* rp = rec + (size_t)ppar * D * 8;
                 const double* pdp = pdl + (size_t)ppar * D;
                 const float* co = cring + (size_t)((i + 3) & 3) * LY::cs;   // node i-1
-                float* cv = cvw + (size_t)(i > 0 ? i - 1 : 0) * DD;
+                float* cv = cst + (size_t)(i & 1) * LY::cs;                  // node i-1, staged
 #pragma unroll
                 for (int q = 0; q < LTQ; ++q) {
                     const bool ok = lk[q] >= 0;
@@ -932,6 +951,10 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             if (hw <= 2 && i + 1 < n) {
                 uint64_t gv = 0;
                 if (lane < D) gv = pring[(size_t)((i + 1) & 3) * 128 + lane];
+#ifdef AME_STAMPS
+                STAMP3(1);
+                if (!__all((lane >= D) || (uint32_t)(gv >> 32) == a.epoch)) STAMP3(6);
+#endif
                 gran_finish(i + 1, gv, muL + hw * 64);
                 STAMP3(2);
                 wave_lds_sync3();
@@ -970,22 +993,25 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
 #endif
                 STAMP3(5);
                 // loader: this step's batch -- Y row i+5, covariance of node i+2, old
-                // means of node i+5 (slice t) and i+4 (slice t+1), granules of node i+4
+                // means of node i+5 (slice t) and i+4 (slice t+1)
                 if (hw == 6) {
                     dma_y(i + 5);
                     dma_cov(i + 2);
                     dma_x(i + 5);
                     dma_r(i + 4);
-                    dma_p(i + 4);
                     STAMP3(6);
                 }
             }
             // the batch issued 2 steps ago must have landed before the next step reads it
             if (hw == 6) vm_wait_le(2 * KDMA);
+            // granules of node i+2, read by HF1 next step
+            if (hw == 5) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             STAMP3(9);
             lds_barrier3();
         }
     }
+    // the last node's new covariance (staged by HB in the epilogue step n)
+    if (wave == 5 && n >= 1) flush_cov(n - 1);
     // ---- slice done: release its means, covariances and granules, then flag it
     // for the next sweep (every wave drains its own stores first) ----
     if (a.done != nullptr) {

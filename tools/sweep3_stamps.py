@@ -21,7 +21,7 @@ SRCS = ("ame_sweep.hip", "ame_sweep3.hip", "ame_sweep4.hip", "ame_cov.hip", "ame
         "ame_selftest.hip", "ame_align.hip")
 NAMES = {
     0: ["start", "J+kj", "reduce", "ddone", "2x2+assembly", "publish", "kcnt", "brow", "gcnt", "prep(v,yv)"],
-    1: ["start", "-", "poll", "hf1", "HB", "GEMV", "-", "-", "-", "end"],
+    1: ["start", "pring", "poll", "hf1", "HB", "GEMV", "spin", "-", "-", "end"],
     2: ["start", "HX", "-", "-", "HB", "GEMV", "-", "-", "-", "end"],
     3: ["start", "-", "-", "-", "(no HB)", "GEMV", "DMA", "-", "-", "vmwait"],
 }
@@ -77,7 +77,8 @@ def run():
         for sl, nm in enumerate(NAMES[w]):
             if nm == "-" or st[w, :, sl].max() == 0:
                 continue
-            print(f"  {sl:2d} {nm:14s} {int(np.median(rel[:, sl])):8d}")
+            hit = st[w, :, sl] != 0
+            print(f"  {sl:2d} {nm:14s} {int(np.median(rel[hit, sl])):8d}  ({int(hit.sum())}/16 steps)")
     pr = (pg - pg[:, :1]) / 100.0   # us (100 MHz realtime)
     st0 = (pg[:, 0] - pg[0, 0]) / 100.0
     print("lane start offset (us) at lanes 0,1,2,4,8,16,32,64,127:",
