@@ -306,6 +306,7 @@ def main():
                              f"SMF-{args.variant} fit iteration, lr={args.lr}"),
                 "n_nodes": n, "n_time_total": T_total, "latent_dim": r, "d": d,
                 "variant": args.variant, "parallelism": f"time-sharded x{world}",
+                "sweep_kind": int(vi.engine.sweep_kind),
             },
             "roofline": {"bound": "hbm", "kernel": "sweep", "achieved": sw["achieved_GBs"],
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": sw["frac"],

@@ -139,6 +139,13 @@ int ame_sweep(const ame_dims* dims, const ame_sweep_args* args, void* stream);
 /* 1 when ame_sweep for (n, r) honours done / wait_epoch, else 0. */
 int ame_sweep_orders_slices(int n, int r);
 
+/* Which sweep kernel ame_sweep launches for these dims (diagnostics, tests):
+ * 4 / 3 = the v4 / v3 single-workgroup-per-slice kernels; 22 = v2 with seven
+ * GEMV worker workgroups per slice (the slice's (U,V) block in their
+ * registers); 21 = v2 with the block in HBM; 20 = v2 with it in LDS;
+ * -1 = unsupported dims. */
+int ame_sweep_kind(const ame_dims* dims);
+
 /* Scratch doubles ame_sweep needs in args->work (see the field). */
 long long ame_sweep_work_size(const ame_dims* dims);
 

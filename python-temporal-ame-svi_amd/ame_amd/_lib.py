@@ -47,7 +47,7 @@ class ame_elbo_args(ctypes.Structure):
 
 
 # every symbol include/ame_amd.h declares (checked by tests/test_capi.py)
-EXPORTS = ("ame_pack_y", "ame_sweep", "ame_sweep_work_size", "ame_sweep_orders_slices", "ame_sweep_max_slices", "ame_sweep_lds_bytes", "ame_cov",
+EXPORTS = ("ame_pack_y", "ame_sweep", "ame_sweep_kind", "ame_sweep_work_size", "ame_sweep_orders_slices", "ame_sweep_max_slices", "ame_sweep_lds_bytes", "ame_cov",
            "ame_elbo", "ame_elbo_work_size", "ame_host_register", "ame_host_unregister",
            "ame_peer_alloc", "ame_peer_free", "ame_peer_open", "ame_peer_close",
            "ame_supported_r", "ame_last_error", "ame_version", "ame_align_work_size",
@@ -72,6 +72,8 @@ def _declare(L):
     L.ame_debug_selftest.restype = ctypes.c_int
     L.ame_sweep_orders_slices.argtypes = [ctypes.c_int, ctypes.c_int]
     L.ame_sweep_orders_slices.restype = ctypes.c_int
+    L.ame_sweep_kind.argtypes = [P(ame_dims)]
+    L.ame_sweep_kind.restype = ctypes.c_int
     L.ame_sweep_work_size.argtypes = [P(ame_dims)]
     L.ame_sweep_work_size.restype = ctypes.c_longlong
     L.ame_supported_r.argtypes = [P(ctypes.c_int), ctypes.c_int]

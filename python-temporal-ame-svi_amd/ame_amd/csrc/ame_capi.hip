@@ -9,6 +9,7 @@
 
 int ame_sweep_dispatch(const ame_dims*, const ame_sweep_args*, hipStream_t);
 int ame_sweep_blocks_per_cu(int n, int r);
+long long ame_sweep_v2w_doubles(const ame_dims* dm);
 int ame_sweep3_dispatch(const ame_dims*, const ame_sweep_args*, hipStream_t);
 int ame_sweep3_supported(int n, int r);
 int ame_sweep3_blocks_per_cu(int n, int r);
@@ -173,10 +174,21 @@ int ame_sweep_max_slices(int n, int r) {
 
 int ame_sweep_orders_slices(int n, int r) { return r_supported(r) && use_v3(n, r) ? 1 : 0; }
 
-// v2 with the slice's (U,V) block in HBM: [T_local][n][2r] fp32 in the work buffer
+// v2 with GEMV workers: their partial ring; else v2 with the slice's (U,V)
+// block in HBM: [T_local][n][2r] fp32 in the work buffer
 static long long v2_global_doubles(const ame_dims* d) {
-    if (use_v3(d->n, d->r) || !sweep_lds_layout(d->n, d->r, ame_sweep_force_global()).m_global) return 0;
+    if (use_v3(d->n, d->r)) return 0;
+    if (const long long w = ame_sweep_v2w_doubles(d)) return w;
+    if (!sweep_lds_layout(d->n, d->r, ame_sweep_force_global()).m_global) return 0;
     return ((long long)d->T_local * d->n * 2 * d->r + 1) / 2;
+}
+
+int ame_sweep_kind(const ame_dims* dims) {
+    if (check_dims(dims)) return -1;
+    if (use_v4(dims->n, dims->r)) return 4;
+    if (use_v3(dims->n, dims->r)) return 3;
+    if (ame_sweep_v2w_doubles(dims) > 0) return 22;
+    return sweep_lds_layout(dims->n, dims->r, ame_sweep_force_global()).m_global ? 21 : 20;
 }
 
 long long ame_sweep_work_size(const ame_dims* dims) {

@@ -91,7 +91,7 @@ __host__ __device__ inline SweepLds sweep_lds_layout(int n, int R, int force_glo
     L.oSsq = o;  o = ame_align16(o + 8LL * (2 * R + D));
     L.oF = o;    o = ame_align16(o + 4LL * 5 * D);
     L.oPart = o; o = ame_align16(o + 4LL * GW * (M2 + 2));
-    L.oZ = o;    o = ame_align16(o + 8LL * n);
+    L.oZ = o;    o = ame_align16(o + 8LL * (n > 2 * D ? n : 2 * D));   // z row, or (workers) new-mean ring
     L.oM = o;
     const long long withM = ame_align16(o + 4LL * n * M2);
     L.m_global = (force_global || withM > AME_LDS_MAX) ? 1 : 0;

@@ -31,6 +31,14 @@
 //      2 wave 0: reductions, 2x2 solves, mu_i, publish ;
 //        waves 1-3: GEMV for node i+1, poll mu_{i+1,t-1}, load mu_{i+1,t+1}
 //      3 all   : K rank-4 update + covariance write ; AR terms of node i+1
+//  * GEMV workers (MODE 2): when the chip has room, the h_obs
+//    GEMV leaves the slice's workgroup.  AME_GW workgroups per slice (other
+//    CUs) each own a node range of the slice's (U,V) block in registers and
+//    publish, per node m, the partial sum over their range with the nodes
+//    m-3..m left out, as {tag, value} granules in a ring.  They use node j's
+//    new mean once the slice's own hand-off granules show it (j <= m-4).  The
+//    slice's workgroup adds the partials in a fixed order plus nodes m-3, m-2
+//    (new means, LDS ring); node m-1 stays the Woodbury observation.
 #include "ame_common.h"
 
 #ifdef AME_STAMPS
@@ -65,6 +73,9 @@ extern "C" int ame_debug_read_stamps(unsigned long long* host, int count) {
 #endif
 
 #define AME_YPF 8   // Y-row prefetch registers per thread (n <= 2048 fully prefetched)
+#define AME_GW 7          // GEMV workers per slice (MODE 2)
+#define AME_GW_RING 8     // partial ring slots per worker
+#define AME_GW_MAXPW 152  // nodes per worker wave held in registers: n <= 7 * 4 * 152
 #ifndef AME_MG_UNROLL
 #define AME_MG_UNROLL 8   // GEMV rows in flight per thread when the slice is read from HBM
 #endif
@@ -137,6 +148,115 @@ __device__ __forceinline__ void tri_decode(int e, int& k, int& m) {
     m = e - k * (k + 1) / 2;
 }
 
+// GEMV worker (MODE 2): workgroup TL + t*AME_GW + g owns nodes
+// [g*NW, (g+1)*NW) of slice t, NW = ceil(n / AME_GW); wave q holds nodes
+// base + q + 4s (s < AME_GW_MAXPW), lane c column c of (U,V), in registers.
+// Per node m it publishes (ring slot m % 8, tag = epoch16 << 16 | m16)
+//   part[c'] = sum_{j in range, j not in [m-3, m]} z_mj . [V | U]_j   (c' < 2r)
+//   part[2r + p] = sum z_mj[p]
+// with node j's new mean for j <= m-4 (read from the slice's hand-off
+// granules, which the slice's workgroup stores when it publishes node j).
+template <int R>
+__device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_args& a, char* smem) {
+    constexpr int D = 2 + 2 * R, M2 = 2 * R, PW = M2 + 2;
+    const int n = dm.n, TL = dm.T_local;
+    const int w = (int)blockIdx.x - TL, t = w / AME_GW, g = w - t * AME_GW;
+    const int NW = (n + AME_GW - 1) / AME_GW, base = g * NW;
+    const int cnt = max(0, min(n, base + NW) - base);
+    const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6;
+    const int npw = (cnt > q) ? (cnt - q + 3) / 4 : 0;
+    float2* zb = (float2*)smem;                                   // [NW] z of the range
+    float* red = (float*)(smem + ame_align16(8LL * NW));           // [4][PW]
+    const float* xo = a.x_old + (size_t)t * n * D;
+    const uint64_t* hand = a.hand + (size_t)t * n * D;
+    uint64_t* hp = (uint64_t*)a.work + (size_t)(t * AME_GW + g) * AME_GW_RING * PW;
+    const float* ysl = a.Yt + (size_t)t * n * n * 2;
+    const float r00f = (float)a.rinv[0], r01f = (float)a.rinv[1], r10f = (float)a.rinv[2], r11f = (float)a.rinv[3];
+    const uint32_t etag = (a.epoch & 0xFFFFu) << 16;
+    const bool col = lane < M2;
+    bool dead = false;
+    float mreg[AME_GW_MAXPW];
+#pragma unroll
+    for (int s2 = 0; s2 < AME_GW_MAXPW; ++s2) {
+        const int j = base + q + 4 * s2;
+        mreg[s2] = (s2 < npw && col) ? xo[(size_t)j * D + 2 + lane] : 0.f;
+    }
+    for (int m = 0; m < n; ++m) {
+        // node m-4's new mean replaces its old one (owner wave); every worker
+        // waits for it (wave 0 of a non-owner polls one granule), which also
+        // keeps it at most 4 nodes ahead of the slice: ring slot m % 8 is free
+        const int jn = m - 4;
+        const bool own = jn >= base && jn < base + cnt;
+        if (jn >= 0 && ((own && ((jn - base) & 3) == q) || (!own && q == 0))) {
+            const int sn = own ? (jn - base) >> 2 : -1;
+            const bool need = own ? col : lane == 0;
+            uint64_t v = 0;
+            bool ok = true;
+            if (need) {
+                v = gran_load_agent(hand + (size_t)jn * D + 2 + lane);
+                ok = (uint32_t)(v >> 32) == a.epoch;
+            }
+            if (!__all(ok) && !dead) {
+                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                while (true) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (need) {
+                        v = gran_load_agent(hand + (size_t)jn * D + 2 + lane);
+                        ok = (uint32_t)(v >> 32) == a.epoch;
+                    }
+                    if (__all(ok)) break;
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > AME_SPIN_TICKS_LOCAL) {
+                        if (lane == 0) atomicOr(a.status, AME_STATUS_SPIN_TIMEOUT);
+#ifdef AME_WDEBUG
+                        if (lane == 0)
+                            printf("worker t=%d g=%d m=%d jn=%d q=%d: granule epoch %u want %u\n", t, g, m, jn,
+                                   q, (uint32_t)(v >> 32), a.epoch);
+#endif
+                        dead = true;
+                        break;
+                    }
+                }
+            }
+            const float val = __uint_as_float((uint32_t)v);
+#pragma unroll
+            for (int s2 = 0; s2 < AME_GW_MAXPW; ++s2)
+                if (s2 == sn && col) mreg[s2] = val;
+        }
+        // z row of node m over the range (nodes m-3..m left out)
+        const float2* yrow = (const float2*)(ysl + (size_t)m * n * 2) + base;
+        for (int e = tid; e < cnt; e += AME_NT) {
+            const float2 y = yrow[e];
+            const int j = base + e;
+            const bool ex = (j >= m - 3) && (j <= m);
+            zb[e] = ex ? make_float2(0.f, 0.f)
+                       : make_float2(r00f * y.x + r01f * y.y, r10f * y.x + r11f * y.y);
+        }
+        __syncthreads();
+        float acc = 0.f, s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int s2 = 0; s2 < AME_GW_MAXPW; ++s2) {
+            if (s2 < npw) {
+                const float2 z = zb[q + 4 * s2];
+                acc = fmaf(lane < R ? z.y : z.x, mreg[s2], acc);   // U_c -> h_V (z1), V -> h_U (z0)
+                s0 += z.x;
+                s1 += z.y;
+            }
+        }
+        if (col) red[q * PW + (lane < R ? R + lane : lane - R)] = acc;
+        if (lane == 0) {
+            red[q * PW + M2] = s0;
+            red[q * PW + M2 + 1] = s1;
+        }
+        __syncthreads();
+        if (tid < PW) {
+            const float v = ((red[tid] + red[PW + tid]) + red[2 * PW + tid]) + red[3 * PW + tid];
+            const uint32_t tag = etag | ((uint32_t)m & 0xFFFFu);
+            gran_store_agent(hp + (size_t)(m % AME_GW_RING) * PW + tid,
+                             ((uint64_t)tag << 32) | (uint64_t)__float_as_uint(v));
+        }
+    }
+}
+
 // MG = false: the slice's (U,V) block lives in LDS (M).  MG = true: it lives in
 // a compact HBM copy (a.work, [T_local][n][2R] fp32, 16-byte aligned rows)
 // that wave 0 updates when it publishes a new mean; wave 0 drains its stores
@@ -144,9 +264,12 @@ __device__ __forceinline__ void tri_decode(int e, int& k, int& m) {
 // workgroup-scope release of the AMDGPU memory model (one CU, shared vL1D).
 // Old values the step itself needs (node i-1 in phase 1, node i in phase 3)
 // come from x_old in that mode.
-template <int R, bool MG>
+// MODE 0: (U,V) in LDS; MODE 1: in HBM (MG); MODE 2: GEMV workers (no slice
+// block in this workgroup at all; old rows of single nodes come from x_old).
+template <int R, int MODE>
 __global__ void __launch_bounds__(AME_NT)
 ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
+    constexpr bool MG = MODE == 1, WK = MODE == 2;
     constexpr int D = 2 + 2 * R, M2 = 2 * R, KS = D + 1, US = (M2 + 15) / 16;
     constexpr int KH = (D + 63) / 64;   // state rows per solver lane
     constexpr int VEC = (R % 4 == 0) ? 4 : ((R % 2 == 0) ? 2 : 1);
@@ -156,12 +279,18 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     static_assert(D <= 128 && 128 + D <= AME_NT && NPA * D <= AME_NT, "sweep v2: D too large");
     constexpr int NLT = D * (D + 1) / 2, LTQ = (NLT + AME_NT - 1) / AME_NT;
     const int n = dm.n, TL = dm.T_local, Tt = dm.T_total;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    if constexpr (WK) {
+        if ((int)blockIdx.x >= TL) {
+            gemv_worker<R>(dm, a, smem);
+            return;
+        }
+    }
     const int tl = blockIdx.x, tg = dm.t_begin + tl;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const bool is_naive = dm.variant == AME_NAIVE, is_bad = dm.variant == AME_BAD;
 
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const SweepLds L = sweep_lds_layout(n, R, MG ? 1 : 0);
+    const SweepLds L = sweep_lds_layout(n, R, MODE != 0 ? 1 : 0);
     double* K = (double*)(smem + L.oK);          // D x KS
     double* vec = (double*)(smem + L.oVec);      // (5+US) x D  K-matvec results
     double* upd = (double*)(smem + L.oUpd);      // 8 x D       rank-4 update vectors
@@ -178,6 +307,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     float* mu_old_n = mu_prev + 4 * D;           // mu_{i+1,t}^old
     float* part = (float*)(smem + L.oPart);      // GW x PW   GEMV partials
     float2* z = (float2*)(smem + L.oZ);          // n         z row of the next node
+    float* mring = (float*)(smem + L.oZ);        // 4 x D     (WK) new means of nodes i & 3
     float* M = (float*)(smem + L.oM);            // n x 2R    (U,V) of the slice (!MG)
 
     const double p = a.rinv[0], s = a.rinv[3], q = 0.5 * (a.rinv[1] + a.rinv[2]);
@@ -200,21 +330,24 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     // (U,V) row of node j as the GEMV sees it (new for nodes already published)
     auto mrow = [&](int j) -> const float* {
         if constexpr (MG) return Mg + (size_t)j * M2;
+        else if constexpr (WK) return xo + (size_t)j * D + 2;   // only asked for old rows
         else return M + j * M2;
     };
     // OLD (U,V) row of node j
     auto mold = [&](int j) -> const float* {
-        if constexpr (MG) return xo + (size_t)j * D + 2;
+        if constexpr (MG || WK) return xo + (size_t)j * D + 2;
         else return M + j * M2;
     };
 
     // ------------------------------------------------------------------
     // init: slice state, P_0 = P_const + sum_{j != 0} F_j, K_0 = P_0^-1
     // ------------------------------------------------------------------
-    for (int idx = tid; idx < n * M2; idx += AME_NT) {
-        const int j = idx / M2, c = idx - j * M2;
-        if constexpr (MG) Mg[idx] = xo[(size_t)j * D + 2 + c];
-        else M[idx] = xo[(size_t)j * D + 2 + c];
+    if constexpr (!WK) {
+        for (int idx = tid; idx < n * M2; idx += AME_NT) {
+            const int j = idx / M2, c = idx - j * M2;
+            if constexpr (MG) Mg[idx] = xo[(size_t)j * D + 2 + c];
+            else M[idx] = xo[(size_t)j * D + 2 + c];
+        }
     }
     if (tid < D) pcd[tid] = pconst_entry(a.consts, D, tid, tid, tg, Tt);
     __syncthreads();
@@ -374,8 +507,57 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     auto gemv_reduce = [&]() {   // threads < PW -> gobs
         if (tid < PW) {
             float acc = 0.f;
-            for (int g = 0; g < GW; ++g) acc += part[g * PW + tid];
+            for (int g = 0; g < (WK ? AME_GW + 1 : GW); ++g) acc += part[g * PW + tid];
             gobs[(tid < M2) ? 2 + tid : tid - M2] = (double)acc;
+        }
+    };
+    // WK, waves 1-3: h_obs partials of `node` from the workers (fixed order),
+    // plus row AME_GW = nodes node-3, node-2 (new means, LDS ring), and the raw
+    // y_{node,node-1} for the Woodbury observation of the next step
+    auto gather = [&](int node) {
+        const int ht = tid - 64;
+        const uint32_t want = ((a.epoch & 0xFFFFu) << 16) | ((uint32_t)node & 0xFFFFu);
+        const uint64_t* hp = (const uint64_t*)a.work + (size_t)tl * AME_GW * AME_GW_RING * PW;
+        for (int e = ht; e < AME_GW * PW; e += 192) {
+            const int g = e / PW, c = e - g * PW;
+            const uint64_t* src = hp + ((size_t)g * AME_GW_RING + (node % AME_GW_RING)) * PW + c;
+            uint64_t v = gran_load_agent(src);
+            if ((uint32_t)(v >> 32) != want && !dead) {
+                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                while (true) {
+                    __builtin_amdgcn_s_sleep(1);
+                    v = gran_load_agent(src);
+                    if ((uint32_t)(v >> 32) == want) break;
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > AME_SPIN_TICKS_LOCAL) {
+                        atomicOr(a.status, AME_STATUS_SPIN_TIMEOUT);
+#ifdef AME_WDEBUG
+                        printf("main tl=%d node=%d g=%d c=%d: tag %x want %x\n", tl, node, g, c,
+                               (uint32_t)(v >> 32), want);
+#endif
+                        dead = true;
+                        break;
+                    }
+                }
+            }
+            part[g * PW + c] = __uint_as_float((uint32_t)v);
+        }
+        if (ht < PW) {
+            float acc = 0.f;
+            for (int j = node - 3; j <= node - 2; ++j) {
+                if (j < 0) continue;
+                const float2 y = *(const float2*)(ysl + ((size_t)node * n + j) * 2);
+                const float z0 = r00f * y.x + r01f * y.y, z1 = r10f * y.x + r11f * y.y;
+                const float* mj = mring + (j & 3) * D;
+                if (ht < R) acc = fmaf(z0, mj[2 + R + ht], acc);          // h_U += z0 V
+                else if (ht < M2) acc = fmaf(z1, mj[2 + ht - R], acc);    // h_V += z1 U
+                else acc += (ht == M2) ? z0 : z1;
+            }
+            part[AME_GW * PW + ht] = acc;
+        }
+        if (ht == 0 && node >= 1) {
+            const float2 y = *(const float2*)(ysl + ((size_t)node * n + node - 1) * 2);
+            scal[40] = (double)y.x;
+            scal[41] = (double)y.y;
         }
     };
     auto ar_terms = [&]() {   // threads < NPA*D: ar = QiPhi mu_left + PhiTQi mu_right
@@ -462,11 +644,11 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     };
 
     // ---- prologue: vectors, g_obs and AR of node 0 ----
-    prefetch_y(0);
+    if constexpr (!WK) prefetch_y(0);
     {
         float nx = 0.f, ol = 0.f;
         if (tid >= 128 && tid < 128 + D) right_regs(0, nx, ol);
-        stage_z(0, -1);
+        if constexpr (!WK) stage_z(0, -1);
         if (wave == 1) {
             if (tg > 0) {
                 uint64_t g0[KH];
@@ -481,9 +663,12 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             mu_old[tid - 128] = ol;
         }
     }
-    if (n > 1) prefetch_y(1);
+    if (!WK && n > 1) prefetch_y(1);
     __syncthreads();
-    if (wave >= 1) gemv(tid - 64);
+    if (wave >= 1) {
+        if constexpr (WK) gather(0);
+        else gemv(tid - 64);
+    }
     __syncthreads();
     gemv_reduce();
     ar_terms();
@@ -513,7 +698,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         if (has_prev && tid < M2) {   // node i-1: statistics and slice (U,V) <- new
             const double vo = (double)mold(i - 1)[tid], vn = (double)mu_prev[2 + tid];
             ssq[tid] = ssq[tid] - vo * vo + vn * vn;
-            if constexpr (!MG) M[(i - 1) * M2 + tid] = mu_prev[2 + tid];
+            if constexpr (MODE == 0) M[(i - 1) * M2 + tid] = mu_prev[2 + tid];
         }
         {
             constexpr int NIT = 4 * D + (1 + US) * D;
@@ -550,7 +735,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             STAMPW(4, 0);
             STAMPW(5, 128);
             STAMPW(6, 192);
-            if (has_next) stage_z(i + 1, i);
+            if (!WK && has_next) stage_z(i + 1, i);
             STAMPW(7, 0);
         }
         // MG: node i-1's (U,V) row (stored by wave 0 in the previous step) is
@@ -665,6 +850,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                         if (k >= 2) Mg[(size_t)i * M2 + (k - 2)] = nw;
                     }
                     mu_prev[k] = nw;
+                    if constexpr (WK) mring[(i & 3) * D + k] = nw;
                     const uint64_t g = ((uint64_t)a.epoch << 32) | (uint64_t)__float_as_uint(nw);
                     gran_store_agent(a.hand + ((size_t)tl * n + i) * D + k, g);
                     if (tl == TL - 1 && a.halo_out != nullptr)
@@ -711,8 +897,12 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             if (tid >= 128 && tid < 128 + D) right_regs(i + 1, nx, ol);
             uint64_t g0[KH];
             if (wave == 1) first_poll(i + 1, g0);
-            if (i + 2 < n) prefetch_y(i + 2);
-            gemv(tid - 64);
+            if constexpr (WK) {
+                gather(i + 1);
+            } else {
+                if (i + 2 < n) prefetch_y(i + 2);
+                gemv(tid - 64);
+            }
             STAMPW(11, 64);
             STAMPW(13, 128);
             if (wave == 1) {
@@ -725,7 +915,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 mu_old_n[tid - 128] = ol;
             }
         }
-        if (wave == 0 && i + 2 < n && has_next) prefetch_y(i + 2);
+        if (!WK && wave == 0 && i + 2 < n && has_next) prefetch_y(i + 2);
         lds_barrier();   // B2
         STAMP(2);
         // ---------------- phase 3 ----------------
@@ -782,42 +972,79 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     }
 }
 
-template <int R, bool MG>
+static long long worker_lds(int n, int R) {
+    const int NW = (n + AME_GW - 1) / AME_GW;
+    return ame_align16(8LL * NW) + 4LL * 4 * (2 * R + 2);
+}
+static long long mode_lds(int n, int R, int mode) {
+    const long long m = sweep_lds_layout(n, R, mode != 0 ? 1 : 0).total;
+    if (mode != 2) return m;
+    const long long w = worker_lds(n, R);
+    return m > w ? m : w;
+}
+
+template <int R, int MODE>
 static int launch_sweep_t(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {
-    const SweepLds L = sweep_lds_layout(dm->n, R, MG ? 1 : 0);
-    auto kern = ame_sweep_kernel<R, MG>;
-    if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)L.total) != hipSuccess)
+    const long long lds = mode_lds(dm->n, R, MODE);
+    auto kern = ame_sweep_kernel<R, MODE>;
+    if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+        hipSuccess)
         return -2;
-    hipLaunchKernelGGL(kern, dim3(dm->T_local), dim3(AME_NT), (size_t)L.total, st, *dm, *a);
+    int blocks = dm->T_local;
+    if constexpr (MODE == 2) {
+        blocks = dm->T_local * (1 + AME_GW);
+        // partial ring: no stale tag may match (tags carry the low 16 epoch bits)
+        const size_t bytes = (size_t)dm->T_local * AME_GW * AME_GW_RING * (2 * R + 2) * 8;
+        if (hipMemsetAsync(a->work, 0, bytes, st) != hipSuccess) return -3;
+    }
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(AME_NT), (size_t)lds, st, *dm, *a);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-template <int R>
-static int launch_sweep(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {
-    if (sweep_lds_layout(dm->n, R, ame_sweep_force_global()).m_global)
-        return launch_sweep_t<R, true>(dm, a, st);
-    return launch_sweep_t<R, false>(dm, a, st);
-}
-
-template <int R, bool MG>
+template <int R, int MODE>
 static int sweep_occupancy_t(int n) {
-    const SweepLds L = sweep_lds_layout(n, R, MG ? 1 : 0);
-    auto kern = ame_sweep_kernel<R, MG>;
-    if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)L.total) != hipSuccess)
+    const long long lds = mode_lds(n, R, MODE);
+    auto kern = ame_sweep_kernel<R, MODE>;
+    if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+        hipSuccess)
         return 0;
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, AME_NT, (size_t)L.total) !=
-        hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, AME_NT, (size_t)lds) != hipSuccess)
         return 0;
     return per_cu;
 }
 
+static bool workers_env_off() {
+    const char* e = getenv("AME_SWEEP_NOWORKERS");
+    return e && e[0] && e[0] != '0';
+}
+
+// MODE 2 when its T_local * (1 + AME_GW) workgroups are co-resident and a
+// worker wave's node share fits its registers
+template <int R>
+static bool use_workers(int n, int T_local) {
+    if (workers_env_off()) return false;
+    const int NW = (n + AME_GW - 1) / AME_GW;
+    if ((NW + 3) / 4 > AME_GW_MAXPW || n > 65535) return false;
+    if (mode_lds(n, R, 2) > AME_LDS_MAX) return false;
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
+    return (long long)T_local * (1 + AME_GW) <= (long long)sweep_occupancy_t<R, 2>(n) * cus;
+}
+
+template <int R>
+static int launch_sweep(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {
+    if (use_workers<R>(dm->n, dm->T_local)) return launch_sweep_t<R, 2>(dm, a, st);
+    if (sweep_lds_layout(dm->n, R, ame_sweep_force_global()).m_global)
+        return launch_sweep_t<R, 1>(dm, a, st);
+    return launch_sweep_t<R, 0>(dm, a, st);
+}
+
 template <int R>
 static int sweep_occupancy(int n) {
-    if (sweep_lds_layout(n, R, ame_sweep_force_global()).m_global) return sweep_occupancy_t<R, true>(n);
-    return sweep_occupancy_t<R, false>(n);
+    if (sweep_lds_layout(n, R, ame_sweep_force_global()).m_global) return sweep_occupancy_t<R, 1>(n);
+    return sweep_occupancy_t<R, 0>(n);
 }
 
 int ame_sweep_dispatch(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {
@@ -834,6 +1061,17 @@ int ame_sweep_blocks_per_cu(int n, int r) {
     switch (r) {
 #define X(RR) \
     case RR: return sweep_occupancy<RR>(n);
+        AME_FOR_EACH_R(X)
+#undef X
+        default: return 0;
+    }
+}
+
+// v2 with GEMV workers: doubles of the partial ring in the work buffer (0 = not used)
+long long ame_sweep_v2w_doubles(const ame_dims* dm) {
+    switch (dm->r) {
+#define X(RR) \
+    case RR: return use_workers<RR>(dm->n, dm->T_local) ? (long long)dm->T_local * AME_GW * AME_GW_RING * (2 * RR + 2) : 0;
         AME_FOR_EACH_R(X)
 #undef X
         default: return 0;

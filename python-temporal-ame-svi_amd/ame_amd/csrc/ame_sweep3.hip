@@ -121,8 +121,10 @@ struct Lay {
     static constexpr int oK = 0;                                   // base inverse, double buffer
     static constexpr int NPA = (4 * D <= 192) ? 4 : 2;
     static constexpr int MCP = ((D + NPA - 1) / NPA) * NPA;       // AR row stride (zero padded)
-    static constexpr int oAR = al16(oK + 8 * 2 * DD);              // Qinv Phi, Phi^T Qinv (fp64) [D][MCP]
-    static constexpr int oRec = al16(oAR + 8 * 2 * D * MCP);       // [par][k]{L0 L1 W0 W1 G0 G1 X0 X1}
+    static constexpr int KS = D + 1;                               // base inverse row stride (odd: no bank conflicts)
+    static constexpr int KSZ = D * KS;
+    static constexpr int oAR = al16(oK + 8 * 2 * KSZ);             // Qinv Phi, Phi^T Qinv (fp64) [D][MCP]
+    static constexpr int oRec = al16(oAR + 8 * 2 * D * MCP);       // [par]{L0 L1 W0 W1 G0 G1 X0 X1}[k]
     static constexpr int oMu64 = al16(oRec + 8 * 2 * D * 8);       // [par][k] new mean (fp64)
     static constexpr int oMu32 = al16(oMu64 + 8 * 2 * D);          // [par][k] new mean (fp32)
     static constexpr int oG = al16(oMu32 + 4 * 2 * D);             // [node&1][k] g of node
@@ -174,7 +176,8 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     using LY = Lay<R>;
     const int YS = LY::ys(n);
-    double* Kbuf = (double*)(smem + LY::oK);
+    double* Kbuf = (double*)(smem + LY::oK);          // [par][k][KS]
+    constexpr int KS = LY::KS, KSZ = LY::KSZ;
     constexpr int MCP = LY::MCP;
     double* arQ = (double*)(smem + LY::oAR);          // Qinv Phi   [D][MCP]
     double* arP = arQ + D * MCP;                       // Phi^T Qinv [D][MCP]
@@ -420,12 +423,12 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 }
             }
             v += pconst_entry(a.consts, D, k, m, tg, Tt);
-            K[k * D + m] = v;
-            K[m * D + k] = v;
+            K[k * KS + m] = v;
+            K[m * KS + k] = v;
         }
         __syncthreads();
         for (int pv = 0; pv < D; ++pv) {   // K -> -P_0^-1
-            if (tid < D) piv[tid] = K[pv * D + tid];
+            if (tid < D) piv[tid] = K[pv * KS + tid];
             __syncthreads();
             const double rinv = 1.0 / piv[pv];
             for (int e = tid; e < NLT; e += kNT) {
@@ -435,13 +438,13 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 if (k == pv && m == pv) v = -rinv;
                 else if (k == pv) v = piv[m] * rinv;
                 else if (m == pv) v = piv[k] * rinv;
-                else v = K[k * D + m] - (piv[k] * piv[m]) * rinv;
-                K[k * D + m] = v;
-                K[m * D + k] = v;
+                else v = K[k * KS + m] - (piv[k] * piv[m]) * rinv;
+                K[k * KS + m] = v;
+                K[m * KS + k] = v;
             }
             __syncthreads();
         }
-        for (int e = tid; e < DD; e += kNT) K[e] = -K[e];
+        for (int e = tid; e < KSZ; e += kNT) K[e] = -K[e];
         __syncthreads();
     }
     for (int e = tid; e < 2 * D * MCP; e += kNT) {   // QiPhi, PhiTQi (adjacent in consts), padded
@@ -658,7 +661,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         const int kc = kl ? k : 0;
         double brow[D];   // row k of the base inverse B_i
 #pragma unroll
-        for (int c = 0; c < D; ++c) brow[c] = kl ? Kbuf[(size_t)k * D + c] : 0.0;
+        for (int c = 0; c < D; ++c) brow[c] = kl ? Kbuf[(size_t)k * KS + c] : 0.0;
         // v = B g, yv = B Jn^T (Jn: J rows of node i+1, old) and this lane's Jn
         // entries, for the coming step; B = brow, g and Jn from HF1 / jn_fill.
         // Runs at the end of the previous step, after the solver's own work.
@@ -777,10 +780,10 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 const V2 s1 = mtv(a1, mv(Mip, b1A)), s2 = mtv(a2, mv(Sip, b2A));
                 const V2 JuA = {eA.x - s1.x + s2.x, eA.y - s1.y + s2.y};
                 // K_i[:, 0:2] (row k) and W_i rows 0, 1 (uniform)
-                const double* r0 = rec + (ppar * D + 0) * 8;
-                const double* r1 = rec + (ppar * D + 1) * 8;
-                const double KE0 = brow[0] - (Lp0 * r0[2] + Lp1 * r0[3]) + (Gp0 * r0[6] + Gp1 * r0[7]);
-                const double KE1 = brow[1] - (Lp0 * r1[2] + Lp1 * r1[3]) + (Gp0 * r1[6] + Gp1 * r1[7]);
+                const double* rq = rec + (size_t)ppar * 8 * D;   // [field][k]
+                const double KE0 = brow[0] - (Lp0 * rq[2 * D] + Lp1 * rq[3 * D]) + (Gp0 * rq[6 * D] + Gp1 * rq[7 * D]);
+                const double KE1 = brow[1] - (Lp0 * rq[2 * D + 1] + Lp1 * rq[3 * D + 1]) +
+                                   (Gp0 * rq[6 * D + 1] + Gp1 * rq[7 * D + 1]);
                 const double WE00 = __shfl(W0, 0), WE01 = __shfl(W1, 0);   // W row 0
                 const double WE10 = __shfl(W0, 1), WE11 = __shfl(W1, 1);   // W row 1
                 const double wz0 = WE00 * zp0 + WE10 * zp1, wz1 = WE01 * zp0 + WE11 * zp1;
@@ -816,9 +819,9 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                     gran_store_system(a.halo_out + (size_t)i * D + k, gr);
                 mu32[par * D + k] = nw;
                 mu64[par * D + k] = (double)nw;
-                double* rc = rec + (par * D + k) * 8;
-                rc[0] = Ln0; rc[1] = Ln1; rc[2] = W0; rc[3] = W1;
-                rc[4] = Gn0; rc[5] = Gn1; rc[6] = Xn0; rc[7] = Xn1;
+                double* rc = rec + (size_t)par * 8 * D + k;   // [field][k]
+                rc[0] = Ln0; rc[D] = Ln1; rc[2 * D] = W0; rc[3 * D] = W1;
+                rc[4 * D] = Gn0; rc[5 * D] = Gn1; rc[6 * D] = Xn0; rc[7 * D] = Xn1;
                 if (is_naive) {
                     const double p = r00, s = r11;
                     double pd;
@@ -840,10 +843,10 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             // next base rows, once every helper wave has written K_i
             lds_wait_ge(kcnt, 7u * (uint32_t)(i + 1), a.status, dead);
             STAMP3(6);
-            const double* Kn = Kbuf + (size_t)ppar * DD;
+            const double* Kn = Kbuf + (size_t)ppar * KSZ;
             if (kl) {
 #pragma unroll
-                for (int c = 0; c < D; ++c) brow[c] = Kn[(size_t)k * D + c];
+                for (int c = 0; c < D; ++c) brow[c] = Kn[(size_t)k * KS + c];
             }
             STAMP3(7);
             if (i + 1 < n) {   // g_{i+1} and Jn of node i+2 from HF1 (hw 0..2)
@@ -875,8 +878,8 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         for (int i = 0; i <= n; ++i) {
             STAMP3(0);
             const int par = i & 1, ppar = (i + 1) & 1;
-            const double* Bi = Kbuf + (size_t)par * DD;      // B_i
-            double* Kn = Kbuf + (size_t)ppar * DD;           // K_i = B_{i+1}
+            const double* Bi = Kbuf + (size_t)par * KSZ;     // B_i
+            double* Kn = Kbuf + (size_t)ppar * KSZ;          // K_i = B_{i+1}
             // new covariance of node i-2 (staged by HB last step): coalesced stores
             // (hw 4: no loads of its own to wait for)
             if (hw == 4 && i >= 2) flush_cov(i - 2);
@@ -888,8 +891,8 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 const int k = lane;
                 const int kc = (k < D) ? k : 0;
                 const double msk = (k < D) ? 1.0 : 0.0;
-                const double* rc = rec + (ppar * D + kc) * 8;
-                const double W0 = msk * rc[2], W1 = msk * rc[3], X0 = msk * rc[6], X1 = msk * rc[7];
+                const double* rc = rec + (size_t)ppar * 8 * D + kc;
+                const double W0 = msk * rc[2 * D], W1 = msk * rc[3 * D], X0 = msk * rc[6 * D], X1 = msk * rc[7 * D];
                 const double g = g64[par * D + kc];
                 double n0, n1;
                 jcol<R>(xring + ((i + 1) & 7) * 64, i + 1 < n, kc, n0, n1);
@@ -907,7 +910,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             }
             // HB (hw 0..5): K_i = B_i - L W^T + G X^T, fused covariance of node i-1
             if (hw <= 5) {
-                const double* rp = rec + (size_t)ppar * D * 8;
+                const double* rp = rec + (size_t)ppar * 8 * D;   // [field][k]
                 const double* pdp = pdl + (size_t)ppar * D;
                 const float* co = cring + (size_t)((i + 3) & 3) * LY::cs;   // node i-1
                 float* cv = cst + (size_t)(i & 1) * LY::cs;                  // node i-1, staged
@@ -915,12 +918,12 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 for (int q = 0; q < LTQ; ++q) {
                     const bool ok = lk[q] >= 0;
                     const int k = ok ? lk[q] : 0, m = ok ? lm[q] : 0;
-                    const double* rk = rp + k * 8;
-                    const double* rm = rp + m * 8;
-                    const double bkm = Bi[k * D + m];
+                    const double* rk = rp + k;
+                    const double* rm = rp + m;
+                    const double bkm = Bi[k * KS + m];
                     const float ckm = co[k * D + m], cmk = co[m * D + k];
-                    const double c = bkm - (rk[0] * rm[2] + rk[1] * rm[3]);
-                    const double kn = c + (rk[4] * rm[6] + rk[5] * rm[7]);
+                    const double c = bkm - (rk[0] * rm[2 * D] + rk[D] * rm[3 * D]);
+                    const double kn = c + (rk[4 * D] * rm[6 * D] + rk[5 * D] * rm[7 * D]);
                     float c32;
                     if (is_naive) {
                         c32 = (k == m) ? 1.0f / ((float)pdp[k] + 1e-8f) : 0.f;
@@ -932,8 +935,8 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                     const float n_km = __fadd_rn(__fmul_rn(lr, c32), __fmul_rn(om, ckm));
                     const float n_mk = __fadd_rn(__fmul_rn(lr, c32), __fmul_rn(om, cmk));
                     if (ok && i < n) {
-                        Kn[k * D + m] = kn;
-                        Kn[m * D + k] = kn;
+                        Kn[k * KS + m] = kn;
+                        Kn[m * KS + k] = kn;
                     }
 #ifndef AME_ABL_NOCOVST
                     if (ok && i >= 1) {

@@ -186,10 +186,6 @@ class DeviceEngine:
             if ws < 0:
                 _lib.check(-1, "ame_elbo_work_size")
             self.work = torch.empty(ws, dtype=torch.float64, device=dev)
-            sws = int(self.L.ame_sweep_work_size(ctypes.byref(self.dims)))
-            if sws < 0:
-                _lib.check(-1, "ame_sweep_work_size")
-            self.sweep_work = torch.empty(max(sws, 1), dtype=torch.float64, device=dev)
             self.out = torch.zeros(8, dtype=torch.float64, device=dev)
             self.status = torch.zeros(1, dtype=torch.int32, device=dev)
         self.epoch = 0
@@ -198,6 +194,16 @@ class DeviceEngine:
             raise RuntimeError(f"ame_amd: no sweep kernel fits n={self.n}, r={self.r}")
         self.groups = slice_groups(sh.T_local, self.max_slices,
                                    int(os.environ.get("AME_SLICE_GROUP", "0")))
+        # the groups of a sweep run one after another and share the scratch
+        sws = 1
+        for size in sorted({sz for _, sz in self.groups}):
+            gd = _lib.ame_dims(self.n, self.r, size, sh.t_begin, sh.T_total, self.vcode)
+            w = int(self.L.ame_sweep_work_size(ctypes.byref(gd)))
+            if w < 0:
+                _lib.check(-1, "ame_sweep_work_size")
+            sws = max(sws, w)
+        self.sweep_work = torch.empty(sws, dtype=torch.float64, device=dev)
+        self.sweep_kind = int(self.L.ame_sweep_kind(ctypes.byref(self.dims)))
         self._out_host = None
         self._out_valid = False
         self.timing = False       # record HIP events around each kernel launch

@@ -1,0 +1,36 @@
+"""Debug build of the v2 GEMV-worker sweep (printf on spin timeouts).
+   python tools/wdebug.py --build   (here)     python tools/wdebug.py  (GPU box)"""
+import os, subprocess, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "python-temporal-ame-svi_amd")
+BDIR = os.path.join(PKG, "ame_amd", "_build")
+SO = os.path.join(BDIR, "libame_amd_wdbg.so")
+SRCS = ("ame_sweep.hip", "ame_sweep3.hip", "ame_sweep4.hip", "ame_cov.hip", "ame_elbo.hip", "ame_capi.hip",
+        "ame_selftest.hip", "ame_align.hip")
+if "--build" in sys.argv:
+    objs = []
+    for src in SRCS:
+        o = os.path.join(BDIR, src.replace(".hip", "_wd.o"))
+        subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17",
+                               "-DAME_WDEBUG", "-DAME_ONLY_R=32", "-Wno-pass-failed", "-c",
+                               os.path.join(PKG, "ame_amd", "csrc", src), "-o", o])
+        objs.append(o)
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", SO, *objs])
+    print("built", SO)
+else:
+    os.environ["AME_LIB_PATH"] = SO
+    sys.path.insert(0, PKG)
+    import torch
+    from ame_amd import TemporalAMEModel, TemporalAMEStructuredMFVI
+    dev = torch.device("cuda", 0)
+    for (n, T) in ((24, 1), (24, 3)):
+        m = TemporalAMEModel(n, T, 32, seed=7)
+        m.generate_data_fast(seed=11)
+        vi = TemporalAMEStructuredMFVI(m, factorization="good", learning_rate=0.5, device=dev)
+        print("kind", vi.engine.sweep_kind, flush=True)
+        try:
+            vi.fit(max_iter=1, tolerance=0.0, verbose=False)
+            print(n, T, "ok", flush=True)
+        except RuntimeError as e:
+            print(n, T, "ERR", e, flush=True)
+        torch.cuda.synchronize()
