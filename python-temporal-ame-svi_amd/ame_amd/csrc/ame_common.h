@@ -72,7 +72,7 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* scratch /* 4*
 // updated this sweep, old ones after), and it takes no LDS.
 #define AME_LDS_MAX 163840LL
 struct SweepLds {
-    long long oK, oVec, oUpd, oRed, oScal, oG, oSsq, oF, oPart, oZ, oM, total;
+    long long oK, oVec, oUpd, oRed, oScal, oG, oSsq, oF, oPart, oCst, oCob, oZ, oM, total;
     int m_global;
 };
 __host__ __device__ inline long long ame_align16(long long x) { return (x + 15) & ~15LL; }
@@ -87,10 +87,12 @@ __host__ __device__ inline SweepLds sweep_lds_layout(int n, int R, int force_glo
     L.oUpd = o;  o = ame_align16(o + 8LL * 8 * D);
     L.oRed = o;  o = ame_align16(o + 8LL * 16 * D);
     L.oScal = o; o = ame_align16(o + 8LL * 64);
-    L.oG = o;    o = ame_align16(o + 8LL * 2 * D);
+    L.oG = o;    o = ame_align16(o + 8LL * 4 * D);   // [node & 1] {g_obs, AR}
     L.oSsq = o;  o = ame_align16(o + 8LL * (2 * R + D));
-    L.oF = o;    o = ame_align16(o + 4LL * 5 * D);
+    L.oF = o;    o = ame_align16(o + 4LL * 9 * D);   // 5 mean rows + 4-slot old-row ring
     L.oPart = o; o = ame_align16(o + 4LL * GW * (M2 + 2));
+    L.oCst = o;  o = ame_align16(o + 4LL * D * D);   // new covariance of the step, staged
+    L.oCob = o;  o = ame_align16(o + 4LL * D * D);   // old covariance of the step
     L.oZ = o;    o = ame_align16(o + 8LL * (n > 2 * D ? n : 2 * D));   // z row, or (workers) new-mean ring
     L.oM = o;
     const long long withM = ame_align16(o + 4LL * n * M2);

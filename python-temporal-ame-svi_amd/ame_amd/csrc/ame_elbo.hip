@@ -67,9 +67,11 @@ int ame_pack_dispatch(const float* Y, float* Yt, const ame_dims* dm, unsigned lo
 // strip; the column tile's U_J, V_J, a_J, b_J are staged in LDS (double
 // buffered, one barrier per tile).  The products are formed transposed,
 //   G1^T = V_J U_I^T,  G2^T = U_J V_I^T   (v_mfma_f32_16x16x4_f32, exact f32),
-// so each lane's 4 accumulator values are 4 CONSECUTIVE columns j of one row i
-// and its Y values are one 32-byte run, loaded as two 16-byte loads issued for
-// the whole tile before the MFMAs.
+// with the A operand rows permuted so that a lane's 4 accumulator values are
+// columns {2lq, 2lq+1, 8+2lq, 9+2lq} of one row i: its Y values are two 16-byte
+// loads and the 4 lanes of a row cover 64 contiguous bytes.  Y streams in half
+// tiles (two 16x16 sub-tiles) through two rotating register buffers, so the
+// next half is in flight while the current one is consumed.
 // ---------------------------------------------------------------------------
 #define AME_TILE 64
 

@@ -40,6 +40,7 @@
 //    slice's workgroup adds the partials in a fixed order plus nodes m-3, m-2
 //    (new means, LDS ring); node m-1 stays the Woodbury observation.
 #include "ame_common.h"
+#include "ame_sweep_dev.h"
 
 #ifdef AME_STAMPS
 // Diagnostic build only (cdna_hip_programming.md §7, in-kernel stamps): lane
@@ -59,11 +60,29 @@ __device__ unsigned long long g_ame_stamps[16 * AME_STAMP_NPH];
             g_ame_stamps[(i - AME_STAMP_I0) * AME_STAMP_NPH + (ph)] = t_;                  \
         }                                                                                  \
     } while (0)
+// GEMV worker 0 of the middle slice: per node m in [I0+4, I0+20): loop top,
+// node m-4 seen, z staged, GEMV done, partial stored
+__device__ unsigned long long g_ame_wstamps[16 * 8];
+#define WSTAMP(ph)                                                                         \
+    do {                                                                                   \
+        if (t == TL / 2 && g == 0 && tid == 0 && m >= AME_STAMP_I0 + 4 && m < AME_STAMP_I0 + 20) { \
+            unsigned long long t_;                                                         \
+            __builtin_amdgcn_sched_barrier(0);                                             \
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");     \
+            __builtin_amdgcn_sched_barrier(0);                                             \
+            g_ame_wstamps[(m - AME_STAMP_I0 - 4) * 8 + (ph)] = t_;                         \
+        }                                                                                  \
+    } while (0)
+extern "C" int ame_debug_read_wstamps(unsigned long long* host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ame_wstamps), sizeof(g_ame_wstamps), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
 extern "C" int ame_debug_read_stamps(unsigned long long* host, int count) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ame_stamps), sizeof(unsigned long long) * count,
                                0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #else
+#define WSTAMP(ph) do { } while (0)
 #define STAMP(ph) \
     do {          \
     } while (0)
@@ -165,8 +184,11 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
     const int cnt = max(0, min(n, base + NW) - base);
     const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6;
     const int npw = (cnt > q) ? (cnt - q + 3) / 4 : 0;
-    float2* zb = (float2*)smem;                                   // [NW] z of the range
-    float* red = (float*)(smem + ame_align16(8LL * NW));           // [4][PW]
+    // z of the range; entries past it stay zero, so the GEMV reads every
+    // register slot's z unconditionally (loads can be batched)
+    constexpr int ZN = 4 * AME_GW_MAXPW;
+    float2* zb = (float2*)smem;                                   // [max(NW, ZN)]
+    float* red = (float*)(smem + ame_align16(8LL * (NW > ZN ? NW : ZN)));   // [4][PW]
     const float* xo = a.x_old + (size_t)t * n * D;
     const uint64_t* hand = a.hand + (size_t)t * n * D;
     uint64_t* hp = (uint64_t*)a.work + (size_t)(t * AME_GW + g) * AME_GW_RING * PW;
@@ -181,7 +203,21 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
         const int j = base + q + 4 * s2;
         mreg[s2] = (s2 < npw && col) ? xo[(size_t)j * D + 2 + lane] : 0.f;
     }
+    for (int e = cnt + tid; e < ZN; e += AME_NT) zb[e] = make_float2(0.f, 0.f);
+    // Y row of the next node, prefetched into registers one node ahead
+    constexpr int YQ = (4 * AME_GW_MAXPW + AME_NT - 1) / AME_NT;
+    float2 ypf[YQ];
+    auto y_prefetch = [&](int m) {
+        const float2* yrow = (const float2*)(ysl + (size_t)(m < n ? m : 0) * n * 2) + base;
+#pragma unroll
+        for (int u = 0; u < YQ; ++u) {
+            const int e = tid + AME_NT * u;
+            ypf[u] = (e < cnt) ? yrow[e] : make_float2(0.f, 0.f);
+        }
+    };
+    y_prefetch(0);
     for (int m = 0; m < n; ++m) {
+        WSTAMP(0);
         // node m-4's new mean replaces its old one (owner wave); every worker
         // waits for it (wave 0 of a non-owner polls one granule), which also
         // keeps it at most 4 nodes ahead of the slice: ring slot m % 8 is free
@@ -222,26 +258,48 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
             for (int s2 = 0; s2 < AME_GW_MAXPW; ++s2)
                 if (s2 == sn && col) mreg[s2] = val;
         }
+        WSTAMP(1);
         // z row of node m over the range (nodes m-3..m left out)
-        const float2* yrow = (const float2*)(ysl + (size_t)m * n * 2) + base;
-        for (int e = tid; e < cnt; e += AME_NT) {
-            const float2 y = yrow[e];
-            const int j = base + e;
-            const bool ex = (j >= m - 3) && (j <= m);
-            zb[e] = ex ? make_float2(0.f, 0.f)
-                       : make_float2(r00f * y.x + r01f * y.y, r10f * y.x + r11f * y.y);
+#pragma unroll
+        for (int u = 0; u < YQ; ++u) {
+            const int e = tid + AME_NT * u;
+            if (e < cnt) {
+                const float2 y = ypf[u];
+                const int j = base + e;
+                const bool ex = (j >= m - 3) && (j <= m);
+                zb[e] = ex ? make_float2(0.f, 0.f)
+                           : make_float2(r00f * y.x + r01f * y.y, r10f * y.x + r11f * y.y);
+            }
         }
+        if (m + 1 < n) y_prefetch(m + 1);
         __syncthreads();
-        float acc = 0.f, s0 = 0.f, s1 = 0.f;
+        WSTAMP(2);
+        // U_c -> h_V (z1), V -> h_U (z0); four independent chains
+        float a4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s2 = 0; s2 < AME_GW_MAXPW; ++s2) {
-            if (s2 < npw) {
+            const float2 z = zb[q + 4 * s2];
+            a4[s2 & 3] = fmaf(lane < R ? z.y : z.x, mreg[s2], a4[s2 & 3]);
+        }
+        const float acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+        // sum of z over the wave's nodes: lane l takes slots l, l+64, l+128, then a
+        // fixed xor tree over the wave
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int u = 0; u < (AME_GW_MAXPW + 63) / 64; ++u) {
+            const int s2 = lane + 64 * u;
+            if (s2 < AME_GW_MAXPW) {
                 const float2 z = zb[q + 4 * s2];
-                acc = fmaf(lane < R ? z.y : z.x, mreg[s2], acc);   // U_c -> h_V (z1), V -> h_U (z0)
                 s0 += z.x;
                 s1 += z.y;
             }
         }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            s0 += __shfl_xor(s0, o);
+            s1 += __shfl_xor(s1, o);
+        }
+        WSTAMP(3);
         if (col) red[q * PW + (lane < R ? R + lane : lane - R)] = acc;
         if (lane == 0) {
             red[q * PW + M2] = s0;
@@ -254,6 +312,7 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
             gran_store_agent(hp + (size_t)(m % AME_GW_RING) * PW + tid,
                              ((uint64_t)tag << 32) | (uint64_t)__float_as_uint(v));
         }
+        WSTAMP(4);
     }
 }
 
@@ -274,9 +333,11 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     constexpr int KH = (D + 63) / 64;   // state rows per solver lane
     constexpr int VEC = (R % 4 == 0) ? 4 : ((R % 2 == 0) ? 2 : 1);
     constexpr int CW = M2 / VEC, GW = 192 / CW, PW = M2 + 2;
-    constexpr int NPA = (4 * D <= AME_NT) ? 4 : 2;   // AR row parts
+    // AR row parts; WK: the AR terms run on waves 1-3 (192 threads) in phase 2
+    constexpr int ART = WK ? 192 : AME_NT;
+    constexpr int NPA = (4 * D <= ART) ? 4 : 2;
     constexpr int MC = (D + NPA - 1) / NPA;
-    static_assert(D <= 128 && 128 + D <= AME_NT && NPA * D <= AME_NT, "sweep v2: D too large");
+    static_assert(D <= 128 && 128 + D <= AME_NT && NPA * D <= ART, "sweep v2: D too large");
     constexpr int NLT = D * (D + 1) / 2, LTQ = (NLT + AME_NT - 1) / AME_NT;
     const int n = dm.n, TL = dm.T_local, Tt = dm.T_total;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -296,8 +357,9 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     double* upd = (double*)(smem + L.oUpd);      // 8 x D       rank-4 update vectors
     double* red = (double*)(smem + L.oRed);      // 16 x D      wave-0 reduction scratch
     double* scal = (double*)(smem + L.oScal);    // 64          sums / y_{i+1,i}
-    double* gobs = (double*)(smem + L.oG);       // D           g_obs of the current node
-    double* ar = gobs + D;                       // D           AR terms of the current node
+    double* gobs_b = (double*)(smem + L.oG);     // [node&1] {D g_obs, D AR terms}
+    auto gob = [&](int node) { return gobs_b + (node & 1) * 2 * D; };
+    uint32_t* wsync = (uint32_t*)(scal + 60);    // WK: phase-2 signals of waves 1-3
     double* ssq = (double*)(smem + L.oSsq);      // 2R          sum U^2, sum V^2 (naive diag)
     double* pcd = ssq + 2 * R;                   // D           diag of P_const
     float* mu_prev = (float*)(smem + L.oF);      // mu_{i-1,t}^new (becomes mu_i in phase 2)
@@ -305,7 +367,13 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     float* mu_right = mu_prev + 2 * D;           // mu_{i+1,t+1}^old
     float* mu_old = mu_prev + 3 * D;             // mu_{i,t}^old
     float* mu_old_n = mu_prev + 4 * D;           // mu_{i+1,t}^old
+    // old means of nodes i-1 .. i+2 (slot j & 3), loaded two steps ahead: the
+    // step's single-node reads of old rows never wait on HBM
+    float* oring = mu_prev + 5 * D;
+    auto orow = [&](int j) -> const float* { return oring + (j & 3) * D + 2; };
     float* part = (float*)(smem + L.oPart);      // GW x PW   GEMV partials
+    float* cst = (float*)(smem + L.oCst);        // D x D     new covariance of node i (phase 3)
+    float* cob = (float*)(smem + L.oCob);        // D x D     old covariance of node i (phase 1)
     float2* z = (float2*)(smem + L.oZ);          // n         z row of the next node
     float* mring = (float*)(smem + L.oZ);        // 4 x D     (WK) new means of nodes i & 3
     float* M = (float*)(smem + L.oM);            // n x 2R    (U,V) of the slice (!MG)
@@ -350,6 +418,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         }
     }
     if (tid < D) pcd[tid] = pconst_entry(a.consts, D, tid, tid, tg, Tt);
+    if (tid == 0) *wsync = 0u;
     __syncthreads();
     if (tid < M2) {   // sum of squares over all nodes: ssq[c<R] = sum U_c^2, ssq[R+c] = sum V_c^2
         double acc = 0.0;
@@ -409,13 +478,14 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         K[k * KS + m] = -K[k * KS + m];
     }
 
-    double qiphi[MC], phitqi[MC];   // AR rows: thread (k = tid / NPA, part = tid % NPA)
+    const int at = WK ? tid - 64 : tid;   // AR thread index
+    double qiphi[MC], phitqi[MC];   // AR rows: thread (k = at / NPA, part = at % NPA)
     {
-        const int k = tid / NPA, pp = tid % NPA;
+        const int k = at / NPA, pp = at % NPA;
 #pragma unroll
         for (int mm = 0; mm < MC; ++mm) {
             const int m = pp * MC + mm;
-            const bool ok = (tid < NPA * D) && (m < D);
+            const bool ok = (at >= 0) && (at < NPA * D) && (m < D);
             qiphi[mm] = ok ? a.consts[3 * DD + (size_t)k * D + m] : 0.0;
             phitqi[mm] = ok ? a.consts[4 * DD + (size_t)k * D + m] : 0.0;
         }
@@ -504,42 +574,65 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             }
         }
     };
-    auto gemv_reduce = [&]() {   // threads < PW -> gobs
-        if (tid < PW) {
+    auto gemv_reduce = [&](int node) {   // threads (WK: 64 +) < PW -> g_obs of node
+        const int rt = WK ? tid - 64 : tid;
+        if (rt >= 0 && rt < PW) {
             float acc = 0.f;
-            for (int g = 0; g < (WK ? AME_GW + 1 : GW); ++g) acc += part[g * PW + tid];
-            gobs[(tid < M2) ? 2 + tid : tid - M2] = (double)acc;
+            for (int g = 0; g < (WK ? AME_GW + 1 : GW); ++g) acc += part[g * PW + rt];
+            gob(node)[(rt < M2) ? 2 + rt : rt - M2] = (double)acc;
         }
     };
-    // WK, waves 1-3: h_obs partials of `node` from the workers (fixed order),
+    // WK, waves 2-3 (wave 1 polls the left slice meanwhile; a load queued
+    // behind that poll would wait for it): h_obs partials of `node` from the
+    // workers (fixed order),
     // plus row AME_GW = nodes node-3, node-2 (new means, LDS ring), and the raw
     // y_{node,node-1} for the Woodbury observation of the next step
     auto gather = [&](int node) {
-        const int ht = tid - 64;
+        const int ht = tid - 128;
+        if (ht < 0) return;
         const uint32_t want = ((a.epoch & 0xFFFFu) << 16) | ((uint32_t)node & 0xFFFFu);
         const uint64_t* hp = (const uint64_t*)a.work + (size_t)tl * AME_GW * AME_GW_RING * PW;
-        for (int e = ht; e < AME_GW * PW; e += 192) {
-            const int g = e / PW, c = e - g * PW;
-            const uint64_t* src = hp + ((size_t)g * AME_GW_RING + (node % AME_GW_RING)) * PW + c;
-            uint64_t v = gran_load_agent(src);
-            if ((uint32_t)(v >> 32) != want && !dead) {
-                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-                while (true) {
-                    __builtin_amdgcn_s_sleep(1);
-                    v = gran_load_agent(src);
-                    if ((uint32_t)(v >> 32) == want) break;
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > AME_SPIN_TICKS_LOCAL) {
-                        atomicOr(a.status, AME_STATUS_SPIN_TIMEOUT);
-#ifdef AME_WDEBUG
-                        printf("main tl=%d node=%d g=%d c=%d: tag %x want %x\n", tl, node, g, c,
-                               (uint32_t)(v >> 32), want);
-#endif
-                        dead = true;
-                        break;
+        // every load issued before any is checked: each is a cross-CU round trip
+        constexpr int NE = AME_GW * PW, GE = (NE + 127) / 128;
+        const uint64_t* hs = hp + (size_t)(node % AME_GW_RING) * PW;
+        uint64_t v[GE];
+#pragma unroll
+        for (int u = 0; u < GE; ++u) {
+            const int e = ht + 128 * u, g = e / PW, c = e - g * PW;
+            v[u] = (e < NE) ? gran_load_agent(hs + (size_t)g * AME_GW_RING * PW + c)
+                            : ((uint64_t)want << 32);
+        }
+        bool ok = true;
+#pragma unroll
+        for (int u = 0; u < GE; ++u) ok = ok && (uint32_t)(v[u] >> 32) == want;
+        if (!ok && !dead) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (true) {
+                __builtin_amdgcn_s_sleep(1);
+                ok = true;
+#pragma unroll
+                for (int u = 0; u < GE; ++u) {
+                    const int e = ht + 128 * u, g = e / PW, c = e - g * PW;
+                    if ((uint32_t)(v[u] >> 32) != want) {
+                        v[u] = gran_load_agent(hs + (size_t)g * AME_GW_RING * PW + c);
+                        ok = ok && (uint32_t)(v[u] >> 32) == want;
                     }
                 }
+                if (ok) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > AME_SPIN_TICKS_LOCAL) {
+                    atomicOr(a.status, AME_STATUS_SPIN_TIMEOUT);
+#ifdef AME_WDEBUG
+                    printf("main tl=%d node=%d: partial tags stale (want %x)\n", tl, node, want);
+#endif
+                    dead = true;
+                    break;
+                }
             }
-            part[g * PW + c] = __uint_as_float((uint32_t)v);
+        }
+#pragma unroll
+        for (int u = 0; u < GE; ++u) {
+            const int e = ht + 128 * u;
+            if (e < NE) part[e] = __uint_as_float((uint32_t)v[u]);   // part[g][c], stride PW
         }
         if (ht < PW) {
             float acc = 0.f;
@@ -560,21 +653,29 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             scal[41] = (double)y.y;
         }
     };
-    auto ar_terms = [&]() {   // threads < NPA*D: ar = QiPhi mu_left + PhiTQi mu_right
-        if (tid < NPA * D) {
-            const int k = tid / NPA, pp = tid % NPA;
-            double acc = 0.0;
+    auto ar_terms = [&](int node) {   // AR threads < NPA*D: QiPhi mu_left + PhiTQi mu_right
+        if (at >= 0 && at < NPA * D) {
+            const int k = at / NPA, pp = at % NPA;
+            // all LDS reads first, then two independent FMA chains
+            float ml[MC], mr[MC];
 #pragma unroll
             for (int mm = 0; mm < MC; ++mm) {
                 const int m = pp * MC + mm;
-                if (m < D) {
-                    if (tg > 0) acc = fma(qiphi[mm], (double)mu_left[m], acc);
-                    if (tg < Tt - 1) acc = fma(phitqi[mm], (double)mu_right[m], acc);
-                }
+                ml[mm] = (m < D) ? mu_left[m] : 0.f;
+                mr[mm] = (m < D) ? mu_right[m] : 0.f;
             }
+            double pL[4] = {0.0, 0.0, 0.0, 0.0}, pR[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int mm = 0; mm < MC; ++mm) {
+                pL[mm & 3] = fma(qiphi[mm], (double)ml[mm], pL[mm & 3]);
+                pR[mm & 3] = fma(phitqi[mm], (double)mr[mm], pR[mm & 3]);
+            }
+            const double aL = (pL[0] + pL[1]) + (pL[2] + pL[3]);
+            const double aR = (pR[0] + pR[1]) + (pR[2] + pR[3]);
+            double acc = ((tg > 0) ? aL : 0.0) + ((tg < Tt - 1) ? aR : 0.0);
             acc += __shfl_xor(acc, 1);
             if constexpr (NPA == 4) acc += __shfl_xor(acc, 2);
-            if (pp == 0) ar[k] = acc;
+            if (pp == 0) gob(node)[D + k] = acc;
         }
     };
     // wave 1: wait for the granules of mu_{node,t-1}^new (returns when done or timed out);
@@ -643,6 +744,37 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         ol = xo[(size_t)node * D + k];
     };
 
+    // Covariances move as whole 16-B rows: the old one of node i+1 is loaded
+    // into registers during step i and parked in LDS at step i+1; the new one of
+    // node i is staged in LDS by phase 3 and stored during step i+1.
+    constexpr int NC4 = D * D / 4;                          // D is even
+    constexpr int CQ = (NC4 + AME_NT - 1) / AME_NT;
+    float4 cpf[CQ];
+    auto cov_prefetch = [&](int node) {
+        const float4* src = (const float4*)(cvs + (size_t)(node < n ? node : 0) * DD);
+#pragma unroll
+        for (int u = 0; u < CQ; ++u) {
+            const int e = tid + AME_NT * u;
+            cpf[u] = (e < NC4) ? src[e] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto cov_park = [&]() {
+#pragma unroll
+        for (int u = 0; u < CQ; ++u) {
+            const int e = tid + AME_NT * u;
+            if (e < NC4) ((float4*)cob)[e] = cpf[u];
+        }
+    };
+    auto cov_flush = [&](int node) {
+        float4* dst = (float4*)(cvw + (size_t)node * DD);
+#pragma unroll
+        for (int u = 0; u < CQ; ++u) {
+            const int e = tid + AME_NT * u;
+            if (e < NC4) dst[e] = ((const float4*)cst)[e];
+        }
+    };
+    cov_prefetch(0);
+
     // ---- prologue: vectors, g_obs and AR of node 0 ----
     if constexpr (!WK) prefetch_y(0);
     {
@@ -662,16 +794,20 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             mu_right[tid - 128] = nx;
             mu_old[tid - 128] = ol;
         }
+        for (int e = tid; e < 2 * D; e += AME_NT) {
+            const int j = e / D, k = e - j * D;
+            oring[j * D + k] = (j < n) ? xo[(size_t)j * D + k] : 0.f;
+        }
     }
     if (!WK && n > 1) prefetch_y(1);
     __syncthreads();
     if (wave >= 1) {
-        if constexpr (WK) gather(0);
+        if constexpr (WK) gather(0);   // waves 2-3
         else gemv(tid - 64);
     }
     __syncthreads();
-    gemv_reduce();
-    ar_terms();
+    gemv_reduce(0);
+    ar_terms(0);
     __syncthreads();
 
     float y_prev0 = 0.f, y_prev1 = 0.f;   // y_{i,i-1} (raw)
@@ -681,26 +817,18 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
 #endif
         STAMP(0);
         const bool has_prev = i > 0, has_next = i + 1 < n;
-        float cold[LTQ], coldT[LTQ];   // old covariance of node i (used in phase 3)
-        {
-            const float* cv = cvs + (size_t)i * DD;
-#pragma unroll
-            for (int qq = 0; qq < LTQ; ++qq) {
-#ifdef AME_ABL_NOCOV
-                cold[qq] = 0.f; coldT[qq] = 0.f; (void)cv;
-#else
-                cold[qq] = (lk[qq] >= 0) ? cv[lk[qq] * D + lm[qq]] : 0.f;
-                coldT[qq] = (lk[qq] >= 0) ? cv[lm[qq] * D + lk[qq]] : 0.f;
-#endif
-            }
-        }
+        if (i >= 1) cov_flush(i - 1);   // staged by phase 3 of step i-1
+        cov_park();                      // old covariance of node i -> cob
+        if (i + 1 < n) cov_prefetch(i + 1);
         // ---------------- phase 1 ----------------
         if (has_prev && tid < M2) {   // node i-1: statistics and slice (U,V) <- new
-            const double vo = (double)mold(i - 1)[tid], vn = (double)mu_prev[2 + tid];
+            const double vo = (double)orow(i - 1)[tid], vn = (double)mu_prev[2 + tid];
             ssq[tid] = ssq[tid] - vo * vo + vn * vn;
             if constexpr (MODE == 0) M[(i - 1) * M2 + tid] = mu_prev[2 + tid];
         }
         {
+            // one item per (row k, vector); independent partial sums so a
+            // wave's dependent FMA chain is short (one wave per SIMD here)
             constexpr int NIT = 4 * D + (1 + US) * D;
             for (int it = tid; it < NIT; it += AME_NT) {
                 double acc = 0.0;
@@ -712,23 +840,33 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                     const bool prevv = qv < 2;
                     if (prevv ? has_prev : has_next) {
                         const bool row0 = (qv & 1) == 0;   // e0 = [1,0,V,0] ; e1 = [0,1,0,U]
-                        const float* src = prevv ? (mu_prev + 2) : mrow(i + 1);
+                        const float* src = prevv ? (mu_prev + 2) : orow(i + 1);
                         const int cb = row0 ? 2 : 2 + R;
                         const float* vv = row0 ? (src + R) : src;
-                        acc = K[k * KS + (row0 ? 0 : 1)];
+                        const double* kr = K + k * KS + cb;
+                        double p4[4] = {K[k * KS + (row0 ? 0 : 1)], 0.0, 0.0, 0.0};
 #pragma unroll
-                        for (int c = 0; c < R; ++c) acc = fma(K[k * KS + cb + c], (double)vv[c], acc);
+                        for (int c = 0; c < R; ++c) p4[c & 3] = fma(kr[c], (double)vv[c], p4[c & 3]);
+                        acc = (p4[0] + p4[1]) + (p4[2] + p4[3]);
                     }
                 } else if (it < 5 * D) {   // u, a-part
                     k = it - 4 * D;
                     slot = 4;
-                    acc = K[k * KS + 0] * (gobs[0] + ar[0]) + K[k * KS + 1] * (gobs[1] + ar[1]);
+                    const double* gi = gob(i);
+                    acc = K[k * KS + 0] * (gi[0] + gi[D]) + K[k * KS + 1] * (gi[1] + gi[D + 1]);
                 } else {                   // u, (U,V)-part chunk
                     const int r2 = it - 5 * D, ch = r2 / D;
                     k = r2 - ch * D;
                     slot = 5 + ch;
-                    const int m0 = 2 + ch * 16, m1 = min(D, m0 + 16);
-                    for (int m = m0; m < m1; ++m) acc = fma(K[k * KS + m], gobs[m] + ar[m], acc);
+                    const int m0 = 2 + ch * 16;
+                    const double* gi = gob(i);
+                    double p2[2] = {0.0, 0.0};
+#pragma unroll
+                    for (int mm = 0; mm < 16; ++mm) {
+                        const int m = m0 + mm;
+                        if (m < D) p2[mm & 1] = fma(K[k * KS + m], gi[m] + gi[D + m], p2[mm & 1]);
+                    }
+                    acc = p2[0] + p2[1];
                 }
                 vec[slot * D + k] = acc;
             }
@@ -750,7 +888,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             // lane owns state rows k = lane + 64h (h < KH)
             double W0[KH], W1[KH], Y0[KH], Y1[KH], ua[KH], uM[KH], gk[KH], K0[KH], K1[KH];
             double jp0[KH], jp1[KH], jn0[KH], jn1[KH];
-            const float* mnext = has_next ? mrow(i + 1) : nullptr;
+            const float* mnext = has_next ? orow(i + 1) : nullptr;
 #pragma unroll
             for (int h = 0; h < KH; ++h) {
                 const int k = lane + 64 * h;
@@ -761,7 +899,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                     ua[h] = vec[4 * D + k];
 #pragma unroll
                     for (int ch = 0; ch < US; ++ch) uM[h] += vec[(5 + ch) * D + k];
-                    gk[h] = gobs[k] + ar[k];
+                    gk[h] = gob(i)[k] + gob(i)[D + k];
                     K0[h] = K[k * KS + 0];
                     K1[h] = K[k * KS + 1];
                     if (k == 0) { jp0[h] = 1.0; jn0[h] = 1.0; }
@@ -894,7 +1032,11 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         } else if (has_next) {
             // waves 1-3: next-node loads first (latency hidden by the GEMV), GEMV, then hand-offs
             float nx = 0.f, ol = 0.f;
-            if (tid >= 128 && tid < 128 + D) right_regs(i + 1, nx, ol);
+            float o2 = 0.f;
+            if (tid >= 128 && tid < 128 + D) {
+                right_regs(i + 1, nx, ol);
+                if (i + 2 < n) o2 = xo[(size_t)(i + 2) * D + (tid - 128)];
+            }
             uint64_t g0[KH];
             if (wave == 1) first_poll(i + 1, g0);
             if constexpr (WK) {
@@ -913,6 +1055,15 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             if (tid >= 128 && tid < 128 + D) {
                 mu_right[tid - 128] = nx;
                 mu_old_n[tid - 128] = ol;
+                oring[((i + 2) & 3) * D + (tid - 128)] = o2;   // node i-2's slot: not read this step
+            }
+            if constexpr (WK) {
+                // partials, mu_{i+1,t-1} and mu_{i+1,t+1} are in LDS once waves 1-3
+                // have signalled: g_obs and the AR terms of node i+1, off phase 3
+                if (lane == 0) ame::lds_signal_add(wsync, 1u);
+                ame::lds_wait_ge(wsync, 3u * (uint32_t)(i + 1), a.status, dead);
+                gemv_reduce(i + 1);
+                ar_terms(i + 1);
             }
         }
         if (!WK && wave == 0 && i + 2 < n && has_next) prefetch_y(i + 2);
@@ -920,7 +1071,6 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         STAMP(2);
         // ---------------- phase 3 ----------------
         {
-            float* cv = cvw + (size_t)i * DD;
 #pragma unroll
             for (int qq = 0; qq < LTQ; ++qq) {
                 const int k = lk[qq], m = lm[qq];
@@ -937,10 +1087,10 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                         if (k == 0) pd = p * (double)(n - 1);
                         else if (k == 1) pd = s * (double)(n - 1);
                         else if (k < 2 + R) {
-                            const double vo = (double)mold(i)[R + (k - 2)];
+                            const double vo = (double)orow(i)[R + (k - 2)];
                             pd = p * (ssq[R + (k - 2)] - vo * vo);
                         } else {
-                            const double uo = (double)mold(i)[k - 2 - R];
+                            const double uo = (double)orow(i)[k - 2 - R];
                             pd = s * (ssq[k - 2 - R] - uo * uo);
                         }
                         c32 = 1.0f / ((float)(pd + pcd[k]) + 1e-8f);
@@ -950,17 +1100,13 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                     if (is_bad && ((k < 2) != (m < 2))) c32 = 0.f;
                     if (k == m) c32 = c32 + 1e-6f;
                 }
-#ifdef AME_ABL_NOCOV
-                if (c32 == 12345.f) cv[0] = c32 + cold[qq] + coldT[qq];
-#else
-                cv[k * D + m] = __fadd_rn(__fmul_rn(lr, c32), __fmul_rn(om, cold[qq]));
-                if (k != m) cv[m * D + k] = __fadd_rn(__fmul_rn(lr, c32), __fmul_rn(om, coldT[qq]));
-#endif
+                cst[k * D + m] = __fadd_rn(__fmul_rn(lr, c32), __fmul_rn(om, cob[k * D + m]));
+                if (k != m) cst[m * D + k] = __fadd_rn(__fmul_rn(lr, c32), __fmul_rn(om, cob[m * D + k]));
             }
             STAMPW(14, 0);
-            if (has_next) {
-                gemv_reduce();
-                ar_terms();
+            if (!WK && has_next) {
+                gemv_reduce(i + 1);
+                ar_terms(i + 1);
             }
             STAMPW(15, 0);
             if (tid >= 128 && tid < 128 + D) mu_old[tid - 128] = mu_old_n[tid - 128];
@@ -970,11 +1116,12 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         lds_barrier();   // B3
         STAMP(3);
     }
+    cov_flush(n - 1);
 }
 
 static long long worker_lds(int n, int R) {
-    const int NW = (n + AME_GW - 1) / AME_GW;
-    return ame_align16(8LL * NW) + 4LL * 4 * (2 * R + 2);
+    const int NW = (n + AME_GW - 1) / AME_GW, ZN = 4 * AME_GW_MAXPW;
+    return ame_align16(8LL * (NW > ZN ? NW : ZN)) + 4LL * 4 * (2 * R + 2);
 }
 static long long mode_lds(int n, int R, int mode) {
     const long long m = sweep_lds_layout(n, R, mode != 0 ? 1 : 0).total;

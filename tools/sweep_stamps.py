@@ -34,7 +34,7 @@ def build(r=16):
     tag = _opt("--tag", "")
     so = SO.replace(".so", f"{tag}.so")
     objs = []
-    for src in ("ame_sweep.hip", "ame_sweep3.hip", "ame_cov.hip", "ame_elbo.hip", "ame_capi.hip",
+    for src in ("ame_sweep.hip", "ame_sweep3.hip", "ame_sweep4.hip", "ame_cov.hip", "ame_elbo.hip", "ame_capi.hip",
                 "ame_selftest.hip", "ame_align.hip"):
         o = os.path.join(BDIR, src.replace(".hip", f"_stamps{tag}.o"))
         subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17",
@@ -86,6 +86,20 @@ def run():
     for ph in sorted(sub):
         d = sum(rows[k][ph] - rows[k][base[ph]] for k in range(15)) / 15
         print(f"    +{d:8.0f} after phase start: {sub[ph]}")
+    if hasattr(L, "ame_debug_read_wstamps"):   # GEMV worker 0 of the same slice (kind 22)
+        L.ame_debug_read_wstamps.argtypes = [ctypes.c_void_p]
+        wb = (ctypes.c_ulonglong * (16 * 8))()
+        if L.ame_debug_read_wstamps(wb) == 0 and wb[0]:
+            w = [[wb[k * 8 + p] for p in range(8)] for k in range(16)]
+            per = [w[k + 1][0] - w[k][0] for k in range(15)]
+            print(f"worker 0: mean node period {sum(per) / 15:.0f} cycles; phases (median over 16 nodes):")
+            for p, nm in enumerate(["node m-4 seen", "z staged", "GEMV done", "partial stored"], 1):
+                d = sorted(w[k][p] - w[k][p - 1] for k in range(16))[8]
+                print(f"    {nm:16s} +{d:7d}")
+            # when partial m (worker) was stored vs main's step m-1 start (node m-1 = I0+3+k)
+            lead = [rows[k + 3][0] - w[k][4] for k in range(13) if rows[k + 3][0]]
+            print("    main step m-1 start minus partial m stored (cycles, >0: ready early):",
+                  sorted(lead)[len(lead) // 2] if lead else None)
 
 
 if __name__ == "__main__":
