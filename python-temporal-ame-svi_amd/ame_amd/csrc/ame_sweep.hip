@@ -73,6 +73,22 @@ __device__ unsigned long long g_ame_wstamps[16 * 8];
             g_ame_wstamps[(m - AME_STAMP_I0 - 4) * 8 + (ph)] = t_;                         \
         }                                                                                  \
     } while (0)
+// phase-2 detail of the middle slice's waves 1-3 (WK): slot = 2 * wave-1 + {0: signalled, 1: reduce+AR done}
+__device__ unsigned long long g_ame_p2stamps[16 * 8];
+#define P2STAMP(sl)                                                                        \
+    do {                                                                                   \
+        if (stamp_on && lane == 0) {                                                       \
+            unsigned long long t_;                                                         \
+            __builtin_amdgcn_sched_barrier(0);                                             \
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");     \
+            __builtin_amdgcn_sched_barrier(0);                                             \
+            g_ame_p2stamps[(i - AME_STAMP_I0) * 8 + (sl)] = t_;                             \
+        }                                                                                  \
+    } while (0)
+extern "C" int ame_debug_read_p2stamps(unsigned long long* host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ame_p2stamps), sizeof(g_ame_p2stamps), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
 extern "C" int ame_debug_read_wstamps(unsigned long long* host) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ame_wstamps), sizeof(g_ame_wstamps), 0,
                                hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
@@ -83,6 +99,7 @@ extern "C" int ame_debug_read_stamps(unsigned long long* host, int count) {
 }
 #else
 #define WSTAMP(ph) do { } while (0)
+#define P2STAMP(sl) do { } while (0)
 #define STAMP(ph) \
     do {          \
     } while (0)
@@ -117,34 +134,24 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 // Wave-0 multi-dot: lane L holds p[h][v] of state rows k = L + 64h < D (KH
-// rows per lane; KH = 2 only for D > 64); every lane gets all NV sums.
-// Reduction: lane L sums red[v][part*QD .. +QD) (v = L>>2, part = L&3, QD =
-// ceil(D/4)), then a 4-lane xor reduction.  NV <= 16.
+// rows per lane; KH = 2 only for D > 64); every lane gets all NV sums.  The
+// lane's rows are added, then one 64-lane reduce-scatter (permlane swaps +
+// DPP, fixed tree: deterministic) leaves sum v on one lane, which writes it
+// to LDS for the others.  NV <= 64.
 template <int NV, int D, int KH>
 __device__ __forceinline__ void wave_multidot(const double (&pv)[KH][NV], double (&out)[NV],
-                                              double* red /* 16*D */, double* sums, int lane) {
-    constexpr int QD = (D + 3) / 4;
+                                              double* red /* unused */, double* sums, int lane) {
+    (void)red;
+    double v[NV];
 #pragma unroll
-    for (int h = 0; h < KH; ++h) {
-        const int k = lane + 64 * h;
-        if (k < D) {
+    for (int q = 0; q < NV; ++q) {
+        v[q] = pv[0][q];
 #pragma unroll
-            for (int v = 0; v < NV; ++v) red[v * D + k] = pv[h][v];
-        }
+        for (int h = 1; h < KH; ++h) v[q] += pv[h][q];
     }
-    wave_lds_sync();
-    const int v = lane >> 2, part = lane & 3;
-    double acc = 0.0;
-    if (v < NV) {
-#pragma unroll
-        for (int k = 0; k < QD; ++k) {
-            const int kk = part * QD + k;
-            if (kk < D) acc += red[v * D + kk];
-        }
-    }
-    acc += __shfl_xor(acc, 1);
-    acc += __shfl_xor(acc, 2);
-    if (v < NV && part == 0) sums[v] = acc;
+    int idx;
+    const double s = ame::wave_reduce_scatter<NV>(v, lane, idx);
+    if (idx < NV) sums[idx] = s;
     wave_lds_sync();
 #pragma unroll
     for (int qq = 0; qq < NV; ++qq) out[qq] = sums[qq];
@@ -817,8 +824,10 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
 #endif
         STAMP(0);
         const bool has_prev = i > 0, has_next = i + 1 < n;
-        if (i >= 1) cov_flush(i - 1);   // staged by phase 3 of step i-1
+        // park first: waiting for last step's prefetch must not also wait for
+        // this step's flush stores (vmcnt counts both, in order)
         cov_park();                      // old covariance of node i -> cob
+        if (i >= 1) cov_flush(i - 1);   // staged by phase 3 of step i-1
         if (i + 1 < n) cov_prefetch(i + 1);
         // ---------------- phase 1 ----------------
         if (has_prev && tid < M2) {   // node i-1: statistics and slice (U,V) <- new
@@ -829,50 +838,94 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         {
             // one item per (row k, vector); independent partial sums so a
             // wave's dependent FMA chain is short (one wave per SIMD here)
-            constexpr int NIT = 4 * D + (1 + US) * D;
-            for (int it = tid; it < NIT; it += AME_NT) {
-                double acc = 0.0;
-                int slot, k;
-                if (it < 4 * D) {   // W0 W1 (node i-1 new) / Y0 Y1 (node i+1 old)
-                    k = it >> 2;
-                    const int qv = it & 3;
-                    slot = qv;
-                    const bool prevv = qv < 2;
-                    if (prevv ? has_prev : has_next) {
-                        const bool row0 = (qv & 1) == 0;   // e0 = [1,0,V,0] ; e1 = [0,1,0,U]
-                        const float* src = prevv ? (mu_prev + 2) : orow(i + 1);
-                        const int cb = row0 ? 2 : 2 + R;
-                        const float* vv = row0 ? (src + R) : src;
-                        const double* kr = K + k * KS + cb;
-                        double p4[4] = {K[k * KS + (row0 ? 0 : 1)], 0.0, 0.0, 0.0};
+            // items: W/Y (one per (row k, vector), R FMAs), u chunks (16 FMAs),
+            // u a-part (2 FMAs).  Independent partial sums keep a wave's
+            // dependent FMA chain short (one wave per SIMD here).
+            auto wy_item = [&](int it) -> double {
+                const int k = it >> 2, qv = it & 3;
+                const bool prevv = qv < 2;
+                if (!(prevv ? has_prev : has_next)) return 0.0;
+                const bool row0 = (qv & 1) == 0;   // e0 = [1,0,V,0] ; e1 = [0,1,0,U]
+                const float* src = prevv ? (mu_prev + 2) : orow(i + 1);
+                const int cb = row0 ? 2 : 2 + R;
+                const float* vv = row0 ? (src + R) : src;
+                const double* kr = K + k * KS + cb;
+                double p4[4] = {K[k * KS + (row0 ? 0 : 1)], 0.0, 0.0, 0.0};
 #pragma unroll
-                        for (int c = 0; c < R; ++c) p4[c & 3] = fma(kr[c], (double)vv[c], p4[c & 3]);
-                        acc = (p4[0] + p4[1]) + (p4[2] + p4[3]);
-                    }
-                } else if (it < 5 * D) {   // u, a-part
-                    k = it - 4 * D;
-                    slot = 4;
-                    const double* gi = gob(i);
-                    acc = K[k * KS + 0] * (gi[0] + gi[D]) + K[k * KS + 1] * (gi[1] + gi[D + 1]);
-                } else {                   // u, (U,V)-part chunk
-                    const int r2 = it - 5 * D, ch = r2 / D;
-                    k = r2 - ch * D;
-                    slot = 5 + ch;
-                    const int m0 = 2 + ch * 16;
-                    const double* gi = gob(i);
-                    double p2[2] = {0.0, 0.0};
+                for (int c = 0; c < R; ++c) p4[c & 3] = fma(kr[c], (double)vv[c], p4[c & 3]);
+                return (p4[0] + p4[1]) + (p4[2] + p4[3]);
+            };
+            auto chunk = [&](int r2) -> double {   // u, (U,V)-part chunk r2 = ch * D + k
+                const int ch = r2 / D, k = r2 - ch * D;
+                const int m0 = 2 + ch * 16;
+                const double* gi = gob(i);
+                double p2[2] = {0.0, 0.0};
 #pragma unroll
-                    for (int mm = 0; mm < 16; ++mm) {
-                        const int m = m0 + mm;
-                        if (m < D) p2[mm & 1] = fma(K[k * KS + m], gi[m] + gi[D + m], p2[mm & 1]);
-                    }
-                    acc = p2[0] + p2[1];
+                for (int mm = 0; mm < 16; ++mm) {
+                    const int m = m0 + mm;
+                    if (m < D) p2[mm & 1] = fma(K[k * KS + m], gi[m] + gi[D + m], p2[mm & 1]);
                 }
-                vec[slot * D + k] = acc;
+                return p2[0] + p2[1];
+            };
+            auto apart = [&](int k) -> double {   // u, a-part
+                const double* gi = gob(i);
+                return K[k * KS + 0] * (gi[0] + gi[D]) + K[k * KS + 1] * (gi[1] + gi[D + 1]);
+            };
+            if constexpr (R == 32 && AME_NT == 256) {
+                // d = 66: 264 W/Y items, 264 chunks, 66 a-parts.  Every round is
+                // one item type per wave (divergent item types in one wave run
+                // back to back): W/Y 0..255, chunks 0..255, then wave 0 splits
+                // the 8 W/Y items of rows 64, 65 into 8 column parts each, wave 1
+                // takes chunks 256..263, waves 2-3 the a-parts.
+                vec[(tid & 3) * D + (tid >> 2)] = wy_item(tid);
+                {
+                    const int ch = tid / D;
+                    vec[(5 + ch) * D + (tid - ch * D)] = chunk(tid);
+                }
+                if (wave == 0) {
+                    const int it = 256 + (lane >> 3), pp = lane & 7;
+                    double v = 0.0;
+                    {   // columns [4 pp, 4 pp + 4) of W/Y item `it`
+                        const int k = it >> 2, qv = it & 3;
+                        const bool prevv = qv < 2, row0 = (qv & 1) == 0;
+                        if (prevv ? has_prev : has_next) {
+                            const float* src = prevv ? (mu_prev + 2) : orow(i + 1);
+                            const float* vv = (row0 ? (src + R) : src) + 4 * pp;
+                            const double* kr = K + k * KS + (row0 ? 2 : 2 + R) + 4 * pp;
+                            double p2[2] = {pp == 0 ? K[k * KS + (row0 ? 0 : 1)] : 0.0, 0.0};
+#pragma unroll
+                            for (int c = 0; c < 4; ++c) p2[c & 1] = fma(kr[c], (double)vv[c], p2[c & 1]);
+                            v = p2[0] + p2[1];
+                        }
+                    }
+                    v += __shfl_xor(v, 1);
+                    v += __shfl_xor(v, 2);
+                    v += __shfl_xor(v, 4);
+                    if (pp == 0) vec[(it & 3) * D + (it >> 2)] = v;
+                } else if (wave == 1) {
+                    if (lane < 8) {
+                        const int r2 = 256 + lane, ch = r2 / D;
+                        vec[(5 + ch) * D + (r2 - ch * D)] = chunk(r2);
+                    }
+                } else {
+                    const int k = tid - 128;
+                    if (k < D) vec[4 * D + k] = apart(k);
+                }
+            } else {
+                constexpr int NIT = 4 * D + (1 + US) * D;
+                for (int it = tid; it < NIT; it += AME_NT) {
+                    if (it < 4 * D) vec[(it & 3) * D + (it >> 2)] = wy_item(it);
+                    else if (it < 5 * D) vec[4 * D + (it - 4 * D)] = apart(it - 4 * D);
+                    else {
+                        const int r2 = it - 5 * D, ch = r2 / D;
+                        vec[(5 + ch) * D + (r2 - ch * D)] = chunk(r2);
+                    }
+                }
             }
             STAMPW(4, 0);
             STAMPW(5, 128);
             STAMPW(6, 192);
+            if (wave == 1) P2STAMP(7);
             if (!WK && has_next) stage_z(i + 1, i);
             STAMPW(7, 0);
         }
@@ -1060,10 +1113,13 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             if constexpr (WK) {
                 // partials, mu_{i+1,t-1} and mu_{i+1,t+1} are in LDS once waves 1-3
                 // have signalled: g_obs and the AR terms of node i+1, off phase 3
+                P2STAMP(2 * (wave - 1));
                 if (lane == 0) ame::lds_signal_add(wsync, 1u);
                 ame::lds_wait_ge(wsync, 3u * (uint32_t)(i + 1), a.status, dead);
+                P2STAMP(6);
                 gemv_reduce(i + 1);
                 ar_terms(i + 1);
+                P2STAMP(2 * (wave - 1) + 1);
             }
         }
         if (!WK && wave == 0 && i + 2 < n && has_next) prefetch_y(i + 2);
