@@ -88,8 +88,18 @@ ame_pairs_kernel(ame_dims dm, const float* __restrict__ Yt, const float* __restr
     const int n = dm.n;
     const int nb = (n + AME_TILE - 1) / AME_TILE;
     const int nws = swap_mode ? (nb + 1) / 2 : nb;     // workgroups per slice
-    const int tl = blockIdx.x / nws;
-    const int s = blockIdx.x - tl * nws;
+    // XCD-aware: workgroup b runs on XCD b % 8; all workgroups of one slice
+    // share an XCD, so its U, V are fetched into one L2 instead of eight
+    const int b = blockIdx.x;
+    int tl, s;
+    if ((dm.T_local & 7) == 0) {
+        const int k = b >> 3, q = k / nws;
+        tl = (b & 7) * (dm.T_local >> 3) + q;
+        s = k - q * nws;
+    } else {
+        tl = b / nws;
+        s = b - tl * nws;
+    }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int li = lane & 15, lq = lane >> 4;
 

@@ -14,3 +14,11 @@ python3 -c "
 import csv
 for r in csv.DictReader(open('$OUT/kernel_stats.csv')):
     if 'ame_' in r['Name']: print(r['Name'][:50], r['Calls'], round(float(r['AverageNs'])/1e3,1), 'us', 'min', round(float(r['MinNs'])/1e3,1))"
+# HBM bytes of the isolated pair kernel (FETCH_SIZE, its own pass)
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex ame_pairs_kernel --output-format csv \
+    -d $OUT/pmc -o pmc -- python3 -u tools/elbo_iso.py --reps 3 > $OUT/pmc.log 2>&1 || { echo "pmc failed"; tail -5 $OUT/pmc.log; exit 1; }
+python3 -c "
+import csv, glob
+v = [float(r['Counter_Value']) for f in glob.glob('$OUT/pmc/**/*counter_collection.csv', recursive=True) for r in csv.DictReader(open(f)) if r['Counter_Name'] == 'FETCH_SIZE']
+v = sorted(v); m = v[len(v)//2] * 1024 * 2   # KiB, x2 on gfx950 (MI355X_MICROARCH.md)
+print('pair kernel HBM read bytes per launch', m, 'vs algorithmic 536346624 ->', round(m / 536346624, 3))"
