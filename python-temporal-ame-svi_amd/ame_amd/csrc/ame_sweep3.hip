@@ -171,7 +171,11 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     const bool is_naive = dm.variant == AME_NAIVE, is_bad = dm.variant == AME_BAD;
     const int ns = (n + kNH - 1) / kNH;
     const int NY = (n * 8 + 1023) / 1024;     // DMA KiB per Y row
+#ifdef AME_S3_OLDP
+    const int KDMA = NY + NC + 3;
+#else
     const int KDMA = NY + NC + 2;             // DMA instructions per step (loader wave)
+#endif
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     using LY = Lay<R>;
@@ -643,12 +647,22 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     __syncthreads();
     if (wave >= 1 && hw <= 2) hf1(0);
     __syncthreads();
-    if (wave == 7) {   // Y rows 2..4 (slots 2,3,0), covariances of nodes 0,1, granules of nodes 1..3
+    if (wave == 7) {   // Y rows 2..4 (slots 2,3,0), covariances of nodes 0,1
         for (int q = 2; q <= 4; ++q) dma_y(q);
         for (int q = 0; q <= 1; ++q) dma_cov(q);
+#ifdef AME_S3_OLDP
         for (int q = 1; q <= 3; ++q) dma_p(q);
+#endif
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+#ifndef AME_S3_OLDP
+    if (wave == 6 && lane < D) {   // granules of node 1 (8-byte atomic loads, see below)
+        uint64_t g1 = 0;
+        if (tg > 0 && n > 1)
+            g1 = (tl == 0) ? gran_load_system(gran_src(1) + lane) : gran_load_agent(gran_src(1) + lane);
+        pring[(size_t)1 * 128 + lane] = g1;
+    }
+#endif
     __syncthreads();
 
     if (wave == 0) {
@@ -883,9 +897,17 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             // new covariance of node i-2 (staged by HB last step): coalesced stores
             // (hw 4: no loads of its own to wait for)
             if (hw == 4 && i >= 2) flush_cov(i - 2);
-            // granules of mu_{i+2,t-1} for HF1 at step i+1: one step ahead only, so
-            // they are current when they land (slice t trails slice t-1 by ~2 steps)
-            if (hw == 5 && i < n) dma_p(i + 2);
+            // hand-off granules of mu_{i+2,t-1} for HF1 at step i+1: one step ahead
+            // only, so they are current when read (slice t trails t-1 by ~2 steps).
+            // Loaded with 8-byte atomic loads, not LDS-DMA: a 16-byte DMA that
+            // races the producer's store may see a granule half-written (new epoch,
+            // old value), which the epoch check cannot tell apart.
+            uint64_t pgr = 0;
+#ifndef AME_S3_OLDP
+            if (hw == 5 && i + 2 < n && tg > 0 && lane < D)
+                pgr = (tl == 0) ? gran_load_system(gran_src(i + 2) + lane)
+                                : gran_load_agent(gran_src(i + 2) + lane);
+#endif
             // HX (hw 5, off the solver's SIMD): dots that do not involve mu_{i-1}
             if (hw == 5 && i < n) {
                 const int k = lane;
@@ -1002,13 +1024,19 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                     dma_cov(i + 2);
                     dma_x(i + 5);
                     dma_r(i + 4);
+#ifdef AME_S3_OLDP
+                    dma_p(i + 4);
+#endif
                     STAMP3(6);
                 }
             }
             // the batch issued 2 steps ago must have landed before the next step reads it
             if (hw == 6) vm_wait_le(2 * KDMA);
-            // granules of node i+2, read by HF1 next step
-            if (hw == 5) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // granules of node i+2, read by HF1 next step (slot (i+2) & 3: not read
+            // this step)
+#ifndef AME_S3_OLDP
+            if (hw == 5 && i < n && lane < D) pring[(size_t)((i + 2) & 3) * 128 + lane] = pgr;
+#endif
             STAMP3(9);
             lds_barrier3();
         }

@@ -275,6 +275,11 @@ ame_sweep4_kernel(ame_dims dm, ame_sweep_args a) {
         if (back_rd) dma4_sys(src + (lane < D ? lane : 0), lds_off(rring + (node & 3) * 64));
         else dma4(src + (lane < D ? lane : 0), lds_off(rring + (node & 3) * 64));
     };
+    // NOTE: a 16-byte LDS-DMA of granules can tear one {epoch, value} pair if it
+    // races the producer's store (v3 therefore reads them with 8-byte atomic
+    // loads, ame_sweep3.hip).  Here the DMA runs 3 steps ahead, where the
+    // granule is either long written or still stale (epoch mismatch -> poll);
+    // v4 is an opt-in experiment.
     auto dma_p = [&](int node) {
         const uint32_t dst = lds_off(pring + (size_t)(node & 3) * 128);
         const int g2 = (lane * 2 < D) ? lane * 2 : 0;
