@@ -85,8 +85,10 @@ typedef struct ame_sweep_args {
     uint32_t epoch;              /* sweep counter, >= 1, identical on every rank */
     uint32_t* status;            /* [1] error word */
     double* work;                /* scratch, >= ame_sweep_work_size() doubles: 0 for the v3
-                                    sweep; [T_local][n][2r] fp32 (U,V) copy when the v2 sweep
-                                    keeps the slice in HBM (n = 4096, r = 32, ...); may be NULL
+                                    sweep; the GEMV workers' partial ring (zeroed by the call
+                                    itself) for v2 with workers (kind 22: n = 4096, r = 32, ...);
+                                    [T_local][n][2r] fp32 (U,V) copy when v2 keeps the slice in
+                                    HBM without workers (kind 21); may be NULL
                                     when the size is 0 */
     float* cov_new;              /* [T_local][n][d][d] damped covariances after the sweep, or NULL
                                     (in place).  A separate buffer lets ame_cov / ame_elbo read
