@@ -188,6 +188,11 @@ def load_pmc(tag):
 
 
 def main():
+    # stdout carries exactly one JSON line: anything a library prints there
+    # (RCCL's version banner at communicator creation, ...) goes to stderr
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -199,6 +204,9 @@ def main():
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=24.0)
+    ap.add_argument("--force-dist", action="store_true",
+                    help="use the process group (nccl) and the time-sharded path even at world size 1 "
+                         "(checks RCCL initialisation on a one-GPU box)")
     args = ap.parse_args()
 
     import torch.distributed as dist
@@ -211,7 +219,8 @@ def main():
     ndev = torch.cuda.device_count()
     dev = torch.device("cuda", local_rank % max(ndev, 1))
     torch.cuda.set_device(dev)
-    if world > 1:
+    use_dist = world > 1 or args.force_dist
+    if use_dist:
         dist.init_process_group("nccl", device_id=dev)
 
     from ame_amd import TemporalAMEModel, TemporalAMENaiveMFVI, TemporalAMEStructuredMFVI
@@ -223,10 +232,10 @@ def main():
     model.generate_data_fast(device=dev)
     if args.variant == "naive":
         vi = TemporalAMENaiveMFVI(model, learning_rate=args.lr, device=dev,
-                                  distributed=world > 1)
+                                  distributed=use_dist)
     else:
         vi = TemporalAMEStructuredMFVI(model, factorization=args.variant, learning_rate=args.lr,
-                                       device=dev, distributed=world > 1)
+                                       device=dev, distributed=use_dist)
     if args.warmup > 0:
         vi.fit(max_iter=args.warmup, tolerance=0.0, verbose=False)
     eng = vi.engine
@@ -234,7 +243,7 @@ def main():
     eng.events.clear()
 
     def barrier():
-        if world > 1:
+        if use_dist:
             dist.barrier()
         torch.cuda.synchronize(dev)
 
@@ -243,7 +252,7 @@ def main():
     hist = vi.fit(max_iter=args.steps, tolerance=0.0, verbose=False)
     barrier()
     dt = time.perf_counter() - t0
-    if world > 1:
+    if use_dist:
         tt = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
@@ -324,8 +333,8 @@ def main():
             "elbo_last": elbo_last,
             "mse_last": float(hist["reconstruction_error"][-1]),
         }
-        print(json.dumps(out))
-    if world > 1:
+        print(json.dumps(out), file=json_out, flush=True)
+    if use_dist:
         dist.barrier()
         dist.destroy_process_group()
     return out
