@@ -9,11 +9,12 @@ import sys
 
 def main():
     out, n, TL = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+    kname = sys.argv[4] if len(sys.argv) > 4 else "ame_sweep"
     vals = {}
     for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if "ame_sweep" not in row["Kernel_Name"]:
+                if kname not in row["Kernel_Name"]:
                     continue
                 key = (row["Counter_Name"], os.path.dirname(f), row["Dispatch_Id"])
                 vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
