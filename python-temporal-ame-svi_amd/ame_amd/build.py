@@ -14,7 +14,23 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libame_amd.so")
 SOURCES = ("ame_sweep.hip", "ame_sweep3.hip", "ame_sweep4.hip", "ame_cov.hip", "ame_elbo.hip", "ame_capi.hip",
-           "ame_selftest.hip", "ame_align.hip")
+           "ame_selftest.hip", "ame_align.hip", "ame_parts.hip")
+# Every latent dim 1..32 is compiled in; the heaviest sources are split into
+# parts by r % parts (ame_common.h AME_R_PART) so the build runs in parallel.
+SPLIT = {"ame_sweep.hip": 3, "ame_sweep3.hip": 2, "ame_elbo.hip": 2}
+
+
+def _units():
+    """(source, object, extra flags) for every translation unit."""
+    out = []
+    for src in SOURCES:
+        parts = SPLIT.get(src, 1)
+        for p in range(parts):
+            if parts == 1:
+                out.append((src, src.replace(".hip", ".o"), []))
+            else:
+                out.append((src, src.replace(".hip", f"_p{p}.o"), [f"-DAME_R_PART={p}", f"-DAME_R_NPART={parts}"]))
+    return out
 ARCH = os.environ.get("AME_OFFLOAD_ARCH", "gfx950")
 
 
@@ -38,21 +54,26 @@ def build(force: bool = False, verbose: bool = True) -> str:
     hipcc = _hipcc()
     bdir = os.path.join(HERE, "_build")
     os.makedirs(bdir, exist_ok=True)
-    objs = [os.path.join(bdir, s.replace(".hip", ".o")) for s in SOURCES]
+    units = _units()
+    objs = [os.path.join(bdir, o) for _, o, _ in units]
     if not force and not _stale(objs):
         return OUT
     flags = [f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-pass-failed"]
 
-    def compile_one(src, obj):
-        cmd = [hipcc, *flags, "-c", os.path.join(CSRC, src), "-o", obj]
+    def compile_one(unit):
+        src, obj, extra = unit
+        cmd = [hipcc, *flags, *extra, "-c", os.path.join(CSRC, src), "-o", os.path.join(bdir, obj)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
-            raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-4000:]}")
+            raise RuntimeError(f"hipcc failed for {src} {extra}:\n{r.stderr[-4000:]}")
         return obj
 
-    jobs = min(len(SOURCES), max(1, min(8, os.cpu_count() or 1)))
+    jobs = min(len(units), max(1, min(16, os.cpu_count() or 1)))
+    # longest units first, so the tail of the parallel build is short
+    order = sorted(units, key=lambda u: -{"ame_sweep.hip": 5, "ame_elbo.hip": 4, "ame_align.hip": 3,
+                                          "ame_sweep3.hip": 2}.get(u[0], 1))
     with cf.ThreadPoolExecutor(jobs) as ex:
-        list(ex.map(lambda so: compile_one(*so), zip(SOURCES, objs)))
+        list(ex.map(compile_one, order))
     tmp = OUT + ".tmp"
     r = subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs],
                        capture_output=True, text=True)

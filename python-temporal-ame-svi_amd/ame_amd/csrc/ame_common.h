@@ -112,6 +112,38 @@ inline int ame_sweep_force_global() {
 // runs on the v2 sweep only (two state rows per lane in the solver wave).
 #ifdef AME_ONLY_R   // diagnostic builds: one latent dim only
 #define AME_FOR_EACH_R(X) X(AME_ONLY_R)
+#elif defined(AME_R_PART)
+// Split build (build.py): the heaviest sources are compiled once per part,
+// part p of AME_R_NPART holding the r with r % AME_R_NPART == p; their
+// r-dependent entry points carry a _p<part> suffix (AME_PFN) and
+// ame_parts.hip routes each call to its part.
+#if AME_R_NPART == 2 && AME_R_PART == 0
+#define AME_FOR_EACH_R(X) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18) X(20) X(22) X(24) X(26) X(28) X(30) X(32)
+#elif AME_R_NPART == 2 && AME_R_PART == 1
+#define AME_FOR_EACH_R(X) X(1) X(3) X(5) X(7) X(9) X(11) X(13) X(15) X(17) X(19) X(21) X(23) X(25) X(27) X(29) X(31)
+#elif AME_R_NPART == 3 && AME_R_PART == 0
+#define AME_FOR_EACH_R(X) X(3) X(6) X(9) X(12) X(15) X(18) X(21) X(24) X(27) X(30)
+#elif AME_R_NPART == 3 && AME_R_PART == 1
+#define AME_FOR_EACH_R(X) X(1) X(4) X(7) X(10) X(13) X(16) X(19) X(22) X(25) X(28) X(31)
+#elif AME_R_NPART == 3 && AME_R_PART == 2
+#define AME_FOR_EACH_R(X) X(2) X(5) X(8) X(11) X(14) X(17) X(20) X(23) X(26) X(29) X(32)
 #else
-#define AME_FOR_EACH_R(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(12) X(16) X(24) X(32)
+#error "AME_R_PART / AME_R_NPART: unsupported split"
+#endif
+#else
+// every latent dim 1..32 (reference: any r, temporal_ame.py:114-120)
+#define AME_FOR_EACH_R(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) \
+    X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32)
+#endif
+#define AME_MAX_R 32
+
+// entry-point names of a split part, and code that only part 0 carries
+#define AME_PFN_CAT2(a, b) a##_p##b
+#define AME_PFN_CAT(a, b) AME_PFN_CAT2(a, b)
+#ifdef AME_R_PART
+#define AME_PFN(name) AME_PFN_CAT(name, AME_R_PART)
+#define AME_PART0 (AME_R_PART == 0)
+#else
+#define AME_PFN(name) name
+#define AME_PART0 1
 #endif

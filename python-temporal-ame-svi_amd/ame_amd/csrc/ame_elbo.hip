@@ -23,6 +23,7 @@ using namespace ame;
 // ---------------------------------------------------------------------------
 // K0: Y [n][n][T_total][2] -> Yt [T_local][n][n][2]; count swap mismatches.
 // ---------------------------------------------------------------------------
+#if AME_PART0
 __global__ void __launch_bounds__(AME_NT)
 ame_pack_kernel(const float* __restrict__ Y, float* __restrict__ Yt, ame_dims dm,
                 unsigned long long* mismatch) {
@@ -58,6 +59,8 @@ int ame_pack_dispatch(const float* Y, float* Yt, const ame_dims* dm, unsigned lo
                        mm);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
+
+#endif
 
 // ---------------------------------------------------------------------------
 // K2: pair terms.  work layout: [nwg][2] = {sum quad (i<j), sum sq-err}
@@ -621,8 +624,8 @@ ame_nodes_kernel(ame_dims dm, const float* __restrict__ x, const float* __restri
         for (int q = 0; q < 6; ++q) partial[(size_t)blockIdx.x * 6 + q] = v[q];
 }
 
-// Final deterministic reduction -> out[8]
-__global__ void __launch_bounds__(AME_NT)
+// Final deterministic reduction -> out[8] (internal linkage: one copy per split part)
+static __global__ void __launch_bounds__(AME_NT)
 ame_final_kernel(const double* __restrict__ p2, int n2, const double* __restrict__ p3, int n3,
                  double* __restrict__ out) {
     __shared__ double red[4 * 8];
@@ -653,9 +656,11 @@ static inline long long nodes_blocks(const ame_dims* dm) {
     return ((long long)dm->T_local * dm->n + AME_NT - 1) / AME_NT;
 }
 
+#if AME_PART0
 long long ame_elbo_work_doubles(const ame_dims* dm) {
     return 2 * pairs_blocks(dm, 0) + 6 * nodes_blocks(dm) + 16;
 }
+#endif
 
 template <int R>
 static int launch_elbo(const ame_dims* dm, const ame_elbo_args* a, hipStream_t st) {
@@ -685,7 +690,7 @@ static int launch_elbo(const ame_dims* dm, const ame_elbo_args* a, hipStream_t s
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-int ame_elbo_dispatch(const ame_dims* dm, const ame_elbo_args* a, hipStream_t st) {
+int AME_PFN(ame_elbo_dispatch)(const ame_dims* dm, const ame_elbo_args* a, hipStream_t st) {
     switch (dm->r) {
 #define X(RR) \
     case RR: return launch_elbo<RR>(dm, a, st);

@@ -1250,7 +1250,7 @@ static int sweep_occupancy(int n) {
     return sweep_occupancy_t<R, 0>(n);
 }
 
-int ame_sweep_dispatch(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {
+int AME_PFN(ame_sweep_dispatch)(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {
     switch (dm->r) {
 #define X(RR) \
     case RR: return launch_sweep<RR>(dm, a, st);
@@ -1260,7 +1260,7 @@ int ame_sweep_dispatch(const ame_dims* dm, const ame_sweep_args* a, hipStream_t 
     }
 }
 
-int ame_sweep_blocks_per_cu(int n, int r) {
+int AME_PFN(ame_sweep_blocks_per_cu)(int n, int r) {
     switch (r) {
 #define X(RR) \
     case RR: return sweep_occupancy<RR>(n);
@@ -1271,7 +1271,7 @@ int ame_sweep_blocks_per_cu(int n, int r) {
 }
 
 // v2 with GEMV workers: doubles of the partial ring in the work buffer (0 = not used)
-long long ame_sweep_v2w_doubles(const ame_dims* dm) {
+long long AME_PFN(ame_sweep_v2w_doubles)(const ame_dims* dm) {
     switch (dm->r) {
 #define X(RR) \
     case RR: return use_workers<RR>(dm->n, dm->T_local) ? (long long)dm->T_local * AME_GW * AME_GW_RING * (2 * RR + 2) : 0;

@@ -880,6 +880,10 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         lds_barrier3();   // epilogue step n
     } else {
         // ============================ HELPERS ============================
+#ifdef AME_S3_HPRIO
+        // diagnostic: helper waves above the waves of kernels running beside the sweep
+        __builtin_amdgcn_s_setprio(AME_S3_HPRIO);
+#endif
         int lk[LTQ], lm[LTQ];
 #pragma unroll
         for (int q = 0; q < LTQ; ++q) {
@@ -1092,7 +1096,7 @@ static int sweep3_occupancy(int n) {
     return per_cu;
 }
 
-int ame_sweep3_blocks_per_cu(int n, int r) {
+int AME_PFN(ame_sweep3_blocks_per_cu)(int n, int r) {
     switch (r) {
 #define X(RR) \
     case RR: if constexpr (RR <= kV3MaxR) return sweep3_occupancy<RR>(n); else return 0;
@@ -1113,7 +1117,7 @@ static int sweep3_fits(int n) {
     return l3_total<R>(n) <= kLDSMAX;
 }
 
-int ame_sweep3_supported(int n, int r) {
+int AME_PFN(ame_sweep3_supported)(int n, int r) {
     switch (r) {
 #define X(RR) \
     case RR: if constexpr (RR <= kV3MaxR) return sweep3_fits<RR>(n); else return 0;
@@ -1134,7 +1138,7 @@ static int launch_sweep3(const ame_dims* dm, const ame_sweep_args* a, hipStream_
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-int ame_sweep3_dispatch(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {
+int AME_PFN(ame_sweep3_dispatch)(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {
     switch (dm->r) {
 #define X(RR) \
     case RR: if constexpr (RR <= kV3MaxR) return launch_sweep3<RR>(dm, a, st); else return -1;
@@ -1144,7 +1148,9 @@ int ame_sweep3_dispatch(const ame_dims* dm, const ame_sweep_args* a, hipStream_t
     }
 }
 
+#if AME_PART0
 long long ame_sweep3_work_doubles(const ame_dims* dm) {
     (void)dm;   // the base inverse lives in LDS (formed in the sweep prologue)
     return 0;
 }
+#endif

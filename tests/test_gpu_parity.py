@@ -124,7 +124,11 @@ def test_single_node_update(gpu_device):
     (20, 1, 2, "good", 1.0), (2, 3, 2, "bad", 0.7), (24, 3, 7, "naive", 1.0),
     (1000, 2, 16, "good", 0.5), (700, 3, 8, "naive", 1.0), (900, 2, 16, "bad", 0.2),
     (60, 3, 12, "good", 0.5), (50, 3, 24, "bad", 0.7), (30, 2, 24, "naive", 1.0),
-    (1200, 1, 24, "good", 0.3)])
+    (1200, 1, 24, "good", 0.3),
+    # latent dims outside round 1's compiled set (each split-build part)
+    (40, 3, 10, "good", 0.5), (30, 2, 13, "naive", 1.0), (26, 3, 20, "bad", 0.7),
+    (20, 2, 31, "good", 0.3), (33, 2, 9, "good", 1.0), (18, 2, 27, "naive", 0.5),
+    (300, 2, 11, "good", 0.5)])
 def test_vs_oracle_fp64(n, T, r, method, lr, gpu_device):
     """Random configurations (odd r, T=1, n=2, ...) against the fp64 oracle.
 
