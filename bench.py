@@ -45,6 +45,8 @@ def kernel_bytes(n, TL, d, swap_consistent=True):
         "cov": 4.0 * n * TL * d * d,
         # Y (upper triangle if swap-consistent) + means
         "elbo": (y_full / 2 if swap_consistent else y_full) + 4.0 * n * TL * d,
+        # the pair kernel alone: the same Y bytes + means
+        "pairs": (y_full / 2 if swap_consistent else y_full) + 4.0 * n * TL * d,
     }
 
 
@@ -169,6 +171,16 @@ def isolated_ms(eng, reps=5):
         eng.launch_elbo()
         torch.cuda.synchronize(eng.dev)
     ms, _ = eng.kernel_ms()
+    # the pair kernel alone (AME_ELBO_PAIRS_ONLY: ame_elbo launches only it)
+    eng.events.clear()
+    os.environ["AME_ELBO_PAIRS_ONLY"] = "1"
+    try:
+        for _ in range(reps):
+            eng.launch_elbo()
+            torch.cuda.synchronize(eng.dev)
+        ms["pairs"] = eng.kernel_ms()[0].get("elbo")
+    finally:
+        del os.environ["AME_ELBO_PAIRS_ONLY"]
     eng.timing = False
     eng.invalidate()
     return ms
@@ -195,8 +207,8 @@ def main():
     os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=1024)
     ap.add_argument("--t-per-gpu", type=int, default=128)
     ap.add_argument("--latent-dim", type=int, default=16)
@@ -276,13 +288,15 @@ def main():
                                "a per-sweep figure)"),
             ("cov", iso.get("cov"), "isolated launch, HIP events on its stream"),
             ("elbo", iso.get("elbo"), "isolated launch (pair + node + final kernels), HIP "
-                                      "events on its stream")):
+                                      "events on its stream"),
+            ("pairs", iso.get("pairs"), "the ELBO pair kernel alone (ame_pairs2_kernel, MFMA), "
+                                        "isolated launch, HIP events on its stream")):
         ent = {"alg_bytes": kb[name], "ms": ms, "timing": how,
                "launch_ms_in_fit": kms.get(name)}
         if ms:
             ach = kb[name] / (ms * 1e-3) / 1e9
             ent.update(achieved_GBs=ach, frac=ach / HBM_PEAK_GBS)
-        pk = pmc.get({"elbo": "pairs"}.get(name, name))
+        pk = pmc.get({"elbo": "pairs"}.get(name, name))   # elbo: its dominant (pair) kernel
         if pk:
             ent["traffic"] = pk.get("hbm_bytes_per_launch")
             ent["traffic_kernel"] = pk.get("kernel")

@@ -23,8 +23,13 @@ struct CovLanes {   // lanes per covariance: next power of two >= 2r
     static constexpr int v = B <= 2 ? 2 : B <= 4 ? 4 : B <= 8 ? 8 : B <= 16 ? 16 : B <= 32 ? 32 : 64;
 };
 
+// Waves per SIMD the register budget must allow (the unrolled elimination
+// otherwise takes 364 VGPRs: one wave per SIMD, latency-bound).
+#ifndef AME_COV_WAVES
+#define AME_COV_WAVES 1
+#endif
 template <int R>
-__global__ void __launch_bounds__(AME_NT)
+__global__ void __launch_bounds__(AME_NT, AME_COV_WAVES)
 ame_cov_kernel(ame_dims dm, ame_cov_args a) {
     constexpr int D = 2 + 2 * R, B = 2 * R, DD = D * D;
     constexpr int LPM = CovLanes<B>::v, MPW = 64 / LPM, WPB = AME_NT / 64;

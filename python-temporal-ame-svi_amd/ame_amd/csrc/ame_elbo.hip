@@ -682,6 +682,10 @@ static int launch_elbo(const ame_dims* dm, const ame_elbo_args* a, hipStream_t s
                                a->x, a->rinv[0], a->rinv[1], a->rinv[2], a->rinv[3],
                                a->swap_consistent, p2);
     }
+    {   // timing knob (bench.py, tools): the pair kernel alone
+        const char* po = getenv("AME_ELBO_PAIRS_ONLY");
+        if (po && po[0] && po[0] != '0') return hipGetLastError() == hipSuccess ? 0 : -3;
+    }
     if (b3 > 0)
         hipLaunchKernelGGL(ame_nodes_kernel<R>, dim3((unsigned)b3), dim3(AME_NT), 0, st, *dm, a->x,
                            a->prev_final, a->cov_terms, a->consts, a->phi, p3);

@@ -91,6 +91,15 @@ namespace {
 
 constexpr int kNT = 512;    // threads per workgroup
 constexpr int kNH = 448;    // helper lanes
+// Node j of the slice's GEMV belongs to helper lane (j + kGOFF) % 448, slot
+// j / 448.  With n > 896 the third slot is partial and, at offset 0, falls on
+// hw 0-1, whose HB + HF1 + GEMV chain is the longest of the step.  Measured at
+// config 3 (profiles/r02_goff.txt): offset 192 (hw 3-4) and 320 (hw 5-6) are
+// no faster (2.75 / 2.77 vs 2.74 ms per iteration), so 0 stays.
+#ifndef AME_S3_GOFF
+#define AME_S3_GOFF 0
+#endif
+constexpr int kGOFF = AME_S3_GOFF;
 constexpr int kMREG = 96;   // VGPR budget for the register-resident part of the node slice
 constexpr int kLDSMAX = 160 * 1024;
 
@@ -168,6 +177,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     const int tg = dm.t_begin + tl;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int hl = tid - 64, hw = wave - 1;   // helper lane / helper wave (valid for wave >= 1)
+    const int hj = (hl + kNH - kGOFF) % kNH;    // first node of helper lane hl (slot 0)
     const bool is_naive = dm.variant == AME_NAIVE, is_bad = dm.variant == AME_BAD;
     const int ns = (n + kNH - 1) / kNH;
     const int NY = (n * 8 + 1023) / 1024;     // DMA KiB per Y row
@@ -468,13 +478,13 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     if (wave >= 1) {
 #pragma unroll
         for (int s = 0; s < NSREG; ++s) {
-            const int j = hl + kNH * s;
+            const int j = hj + kNH * s;
             const bool ok = s < ns && j < n;
 #pragma unroll
             for (int c = 0; c < M2; ++c) mreg[s][c] = ok ? xo[(size_t)j * D + 2 + c] : 0.f;
         }
         for (int s = NSREG; s < ns; ++s) {
-            const int j = hl + kNH * s;
+            const int j = hj + kNH * s;
             const bool ok = j < n;
             for (int c2 = 0; c2 < MP; ++c2) {
                 float2 v = make_float2(0.f, 0.f);
@@ -510,14 +520,14 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         float2 yv[NSREG];
 #pragma unroll
         for (int s = 0; s < NSREG; ++s) {   // ring slots are >= n long: loads need no guard
-            const int j = hl + kNH * s;
+            const int j = hj + kNH * s;
             const float2 y = ysrc[j];
             yv[s] = (j < n) ? y : make_float2(0.f, 0.f);
         }
 #pragma unroll
         for (int s = 0; s < NSREG; ++s) {
             if (s < ns) {
-                const int j = hl + kNH * s;
+                const int j = hj + kNH * s;
                 const bool ex = (j >= m - 2) && (j <= m);
                 const float z0 = ex ? 0.f : r00f * yv[s].x + r01f * yv[s].y;
                 const float z1 = ex ? 0.f : r10f * yv[s].x + r11f * yv[s].y;
@@ -533,7 +543,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             }
         }
         for (int s = NSREG; s < ns; ++s) {
-            const int j = hl + kNH * s;
+            const int j = hj + kNH * s;
             float2 y = ysrc[j];
             if (j >= n) y = make_float2(0.f, 0.f);
             const bool ex = (j >= m - 2) && (j <= m);
@@ -563,12 +573,12 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         if (idx < D) gp[((m & 1) * 7 + hw) * D + idx] = v;
         // raw y_{m,m-1}, y_{m,m-2} for the solver / HF1 (owner lanes only)
         const int jm1 = m - 1, jm2 = m - 2;
-        if (jm1 >= 0 && (jm1 % kNH) == hl) {
+        if (jm1 >= 0 && ((jm1 + kGOFF) % kNH) == hl) {
             const float2 y = ysrc[jm1];
             yst[(m & 3) * 4 + 0] = y.x;
             yst[(m & 3) * 4 + 1] = y.y;
         }
-        if (jm2 >= 0 && (jm2 % kNH) == hl) {
+        if (jm2 >= 0 && ((jm2 + kGOFF) % kNH) == hl) {
             const float2 y = ysrc[jm2];
             yst[(m & 3) * 4 + 2] = y.x;
             yst[(m & 3) * 4 + 3] = y.y;
@@ -995,7 +1005,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             if (i < n) {
                 // M update with mu_{i-1} (owner lane)
                 if (i >= 1) {
-                    const int j = i - 1, so = j / kNH, ho = j - so * kNH;
+                    const int j = i - 1, so = j / kNH, ho = (j - so * kNH + kGOFF) % kNH;
                     if (hl == ho) {
                         const float* mup = mu32 + ppar * D;
                         if (so < NSREG) {

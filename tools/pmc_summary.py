@@ -13,7 +13,7 @@ import os
 import re
 import sys
 
-KERNELS = {"sweep": r"ame_sweep\d?_kernel", "pairs": r"ame_pairs_kernel", "cov": r"ame_cov_kernel"}
+KERNELS = {"sweep": r"ame_sweep\d?_kernel", "pairs": r"ame_pairs2?_kernel", "cov": r"ame_cov_kernel"}
 
 
 def per_launch(outdir, counter):
