@@ -13,7 +13,7 @@ for C in FETCH_SIZE WRITE_SIZE; do
       -d $OUT/pmc_$C -o pmc -- python3 -u bench.py --no-cpu-baseline --steps 3 --warmup 1 \
       > $OUT/pmc_$C.log 2>&1 || { echo "pmc $C failed"; tail -5 $OUT/pmc_$C.log; exit 1; }
 done
-timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex ame_pairs_kernel \
+timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex ame_pairs \
     --output-format csv -d $OUT/pmc_pairs_mfma -o pmc -- python3 -u bench.py --no-cpu-baseline --steps 3 --warmup 1 \
     > $OUT/pmc_pairs_mfma.log 2>&1 || { echo "pmc pairs mfma failed"; tail -5 $OUT/pmc_pairs_mfma.log; exit 1; }
 python3 tools/pmc_pairs.py $OUT > $OUT/pmc_pairs.json || exit 1

@@ -11,7 +11,7 @@ import os
 import sys
 
 
-def per_launch(outdir, sub, counter, kernel="ame_pairs_kernel"):
+def per_launch(outdir, sub, counter, kernel="ame_pairs"):
     vals = {}
     for f in glob.glob(os.path.join(outdir, sub, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
@@ -31,7 +31,7 @@ def main():
     mfma = per_launch(out, "pmc_pairs_mfma", "SQ_VALU_MFMA_BUSY_CYCLES")
     gui = per_launch(out, "pmc_pairs_mfma", "GRBM_GUI_ACTIVE")
     cus = 256
-    res = {"kernel": "ame_pairs_kernel<16> (K3, n=1024, T=128, r=16)",
+    res = {"kernel": "ame_pairs2_kernel<16> (K3, n=1024, T=128, r=16)",
            "hbm_read_bytes_per_launch": None if fetch is None else 2.0 * fetch * 1024.0,
            "algorithmic_read_bytes": 4.0 * 1024 * 1023 * 128,
            "SQ_VALU_MFMA_BUSY_CYCLES": mfma, "GRBM_GUI_ACTIVE": gui}
