@@ -279,7 +279,8 @@ ame_pairs_kernel(ame_dims dm, const float* __restrict__ Yt, const float* __restr
 // flight and the count of outstanding loads is known exactly:
 //  * Y: each wave streams its own 16 rows in half tiles (16 rows x 32 columns =
 //    4 KiB = 4 DMA instructions, each 4 rows x 256 contiguous bytes) through a
-//    private 3-slot LDS ring, two half tiles ahead of the one it computes.
+//    private LDS ring (AME_P2_NSLOT slots), NSLOT - 1 half tiles ahead of the
+//    one it computes.
 //    Within a row the 16-byte chunks are stored XOR-swizzled by the row
 //    (position p holds chunk p ^ row), so the accumulator-order ds_read_b128 of
 //    16 rows hits 16 distinct bank groups; a wave waits only for its own DMA.
@@ -296,19 +297,26 @@ struct Pairs2 {
     static constexpr int SF = 2 * AME_TILE * LD + 2 * AME_TILE;   // staging floats per buffer
     static constexpr int NUV = SF / 64;                             // 4-byte DMA instructions per buffer
     static constexpr int NUW = NUV / 4;                             // ... per wave
-    static constexpr int NSLOT = 3, SLOTB = 4096;
+// 2 slots (one half tile in flight while one is computed) keep the LDS at
+// 50 KB, so 3 workgroups share a CU: 109 us at config 3 vs 117 us with 3 slots
+// and 2 workgroups per CU (profiles/r02_pairs_nslot.txt)
+#ifndef AME_P2_NSLOT
+#define AME_P2_NSLOT 2
+#endif
+    static constexpr int NSLOT = AME_P2_NSLOT, SLOTB = 4096;   // half-tile slots per wave
+    static constexpr int AHEAD = NSLOT - 1;                      // half tiles in flight
     static_assert(SF % 256 == 0, "staging must split evenly over 4 waves");
-    static_assert(8 + NUW <= 63, "vmcnt range");
+    static_assert(4 * AHEAD + NUW <= 63, "vmcnt range");
 };
 
 template <int R>
-__global__ void __launch_bounds__(AME_NT, 2)
+__global__ void __launch_bounds__(AME_NT, (AME_P2_NSLOT <= 2 && R <= 16) ? 3 : 2)
 ame_pairs2_kernel(ame_dims dm, const float* __restrict__ Yt, const float* __restrict__ x,
                   double r00, double r01, double r10, double r11, int swap_mode,
                   double* __restrict__ partial) {
     using P2 = Pairs2<R>;
     constexpr int D = 2 + 2 * R;
-    constexpr int RP = P2::RP, LD = P2::LD, SF = P2::SF, NUW = P2::NUW, NSLOT = P2::NSLOT;
+    constexpr int RP = P2::RP, LD = P2::LD, SF = P2::SF, NUW = P2::NUW, NSLOT = P2::NSLOT, AHEAD = P2::AHEAD;
     const int n = dm.n;
     const int nb = (n + AME_TILE - 1) / AME_TILE;
     const int nws = swap_mode ? (nb + 1) / 2 : nb;
@@ -431,9 +439,9 @@ ame_pairs2_kernel(ame_dims dm, const float* __restrict__ Yt, const float* __rest
     }
 
     issue_uv(0);
-    issue_y(0);
-    issue_y(1);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // staging of tile 0
+#pragma unroll
+    for (int q = 0; q < AHEAD; ++q) issue_y(q);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * AHEAD) : "memory");   // staging of tile 0
     lds_barrier3();   // LDS-only barrier: the Y prefetch stays in flight
 
     // residual sufficient statistics, packed over two columns (v_pk_fma_f32):
@@ -465,12 +473,13 @@ ame_pairs2_kernel(ame_dims dm, const float* __restrict__ Yt, const float* __rest
 #pragma unroll
             for (int hf = 0; hf < 2; ++hf) {
                 const int q = 2 * tt + hf;
-                issue_y(q + 2);
-                // outstanding after half q: half q+1 (4), [hf 0: staging (NUW)], half q+2 (4)
+                issue_y(q + AHEAD);
+                // outstanding after half q: halves q+1 .. q+AHEAD (4 each) and, at
+                // hf 0, the staging of tile tt+1 (NUW); at hf 1 that has landed too
                 if (hf == 0) {
-                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + NUW) : "memory");
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * AHEAD + NUW) : "memory");
                 } else {
-                    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // staging of tile tt+1 landed too
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * AHEAD) : "memory");
                 }
                 const float* ysl = (const float*)&yl[w][q % NSLOT][0] + li * 64;
 #pragma unroll
