@@ -903,10 +903,23 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                     v += __shfl_xor(v, 4);
                     if (pp == 0) vec[(it & 3) * D + (it >> 2)] = v;
                 } else if (wave == 1) {
-                    if (lane < 8) {
-                        const int r2 = 256 + lane, ch = r2 / D;
-                        vec[(5 + ch) * D + (r2 - ch * D)] = chunk(r2);
+                    // chunks 256..263 split 8 ways like wave 0's W/Y items (one
+                    // 16-FMA chunk on 8 lanes made this wave finish phase 1 ~2k
+                    // cycles after the others, profiles/r02_c5_workers_stamps.txt)
+                    const int r2 = 256 + (lane >> 3), pp = lane & 7;
+                    const int ch = r2 / D, k = r2 - ch * D;
+                    const int m0 = 2 + ch * 16 + 2 * pp;
+                    const double* gi = gob(i);
+                    double v = 0.0;
+#pragma unroll
+                    for (int mm = 0; mm < 2; ++mm) {
+                        const int m = m0 + mm;
+                        if (m < D) v = fma(K[k * KS + m], gi[m] + gi[D + m], v);
                     }
+                    v += __shfl_xor(v, 1);
+                    v += __shfl_xor(v, 2);
+                    v += __shfl_xor(v, 4);
+                    if (pp == 0) vec[(5 + ch) * D + k] = v;
                 } else {
                     const int k = tid - 128;
                     if (k < D) vec[4 * D + k] = apart(k);

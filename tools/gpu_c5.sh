@@ -14,4 +14,4 @@ run() {  # variant, extra env
   python3 -c "import json; z=[json.loads(l) for l in open('$OUT/c5.jsonl')][-1]; print('$1 $2', round(z['ms_per_step'],2), 'ms/iter', round(z['ms_per_step']*1000/4096,2), 'us/node-step', z['config'].get('sweep_kind'))"
 }
 for V in naive good bad; do run $V "X=1" || exit 1; done
-run good "AME_SWEEP_NOWORKERS=1" || exit 1
+# (single-workgroup v2 for comparison: run good "AME_SWEEP_NOWORKERS=1")
