@@ -88,7 +88,7 @@ __host__ __device__ inline SweepLds sweep_lds_layout(int n, int R, int force_glo
     L.oRed = o;  o = ame_align16(o + 8LL * 16 * D);
     L.oScal = o; o = ame_align16(o + 8LL * 64);
     L.oG = o;    o = ame_align16(o + 8LL * 4 * D);   // [node & 1] {g_obs, AR}
-    L.oSsq = o;  o = ame_align16(o + 8LL * (2 * R + D));
+    L.oSsq = o;  o = ame_align16(o + 8LL * (2 * R + D) + 4LL * D);   // ssq, diag P_const, naive diag C
     L.oF = o;    o = ame_align16(o + 4LL * 9 * D);   // 5 mean rows + 4-slot old-row ring
     L.oPart = o; o = ame_align16(o + 4LL * GW * (M2 + 2));
     L.oCst = o;  o = ame_align16(o + 4LL * D * D);   // new covariance of the step, staged

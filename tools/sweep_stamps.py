@@ -1,7 +1,7 @@
 """Diagnostic: per-phase cycle shares of one sweep step (in-kernel s_memtime stamps).
 
     python tools/sweep_stamps.py --build [--r=16]          # here: hipcc -DAME_STAMPS -> _build/libame_amd_stamps.so
-    python tools/sweep_stamps.py [--n=1024 --T=128 --r=16] # GPU box: v2 sweep (AME_SWEEP_V2=1), phase shares
+    python tools/sweep_stamps.py [--n=1024 --T=128 --r=16 --variant=good] # GPU box: v2 sweep (AME_SWEEP_V2=1), phase shares
 
 Stamps are taken by thread 0 of the middle lane for 16 nodes in steady state.
 The stamped build's run time is never quoted; only its SHARES are meaningful.
@@ -51,12 +51,16 @@ def run():
     n, T, r = int(_opt("--n", 1024)), int(_opt("--T", 128)), int(_opt("--r", 16))
     sys.path.insert(0, PKG)
     import torch
-    from ame_amd import TemporalAMEModel, TemporalAMEStructuredMFVI
+    from ame_amd import TemporalAMEModel, TemporalAMENaiveMFVI, TemporalAMEStructuredMFVI
     from ame_amd import _lib
     dev = torch.device("cuda", 0)
     m = TemporalAMEModel(n, T, r, seed=42)
     m.generate_data_fast(device=dev)
-    vi = TemporalAMEStructuredMFVI(m, factorization="good", learning_rate=0.01, device=dev)
+    variant = _opt("--variant", "good")
+    if variant == "naive":
+        vi = TemporalAMENaiveMFVI(m, learning_rate=0.01, device=dev)
+    else:
+        vi = TemporalAMEStructuredMFVI(m, factorization=variant, learning_rate=0.01, device=dev)
     vi.fit(max_iter=2, tolerance=0.0, verbose=False)
     torch.cuda.synchronize()
     L = _lib.lib()
