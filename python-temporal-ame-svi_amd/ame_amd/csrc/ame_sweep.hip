@@ -661,6 +661,44 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             scal[41] = (double)y.y;
         }
     };
+    // WK: the PhiTQi mu_right half first (mu_right is in LDS from phase 1 on),
+    // the QiPhi mu_left half once wave 1 has polled mu_left
+    auto ar_right = [&]() -> double {
+        double aR = 0.0;
+        if (at >= 0 && at < NPA * D) {
+            const int pp = at % NPA;
+            float mr[MC];
+#pragma unroll
+            for (int mm = 0; mm < MC; ++mm) {
+                const int m = pp * MC + mm;
+                mr[mm] = (m < D) ? mu_right[m] : 0.f;
+            }
+            double pR[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int mm = 0; mm < MC; ++mm) pR[mm & 3] = fma(phitqi[mm], (double)mr[mm], pR[mm & 3]);
+            aR = (pR[0] + pR[1]) + (pR[2] + pR[3]);
+        }
+        return aR;
+    };
+    auto ar_left_finish = [&](int node, double aR) {
+        if (at >= 0 && at < NPA * D) {
+            const int k = at / NPA, pp = at % NPA;
+            float ml[MC];
+#pragma unroll
+            for (int mm = 0; mm < MC; ++mm) {
+                const int m = pp * MC + mm;
+                ml[mm] = (m < D) ? mu_left[m] : 0.f;
+            }
+            double pL[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int mm = 0; mm < MC; ++mm) pL[mm & 3] = fma(qiphi[mm], (double)ml[mm], pL[mm & 3]);
+            const double aL = (pL[0] + pL[1]) + (pL[2] + pL[3]);
+            double acc = ((tg > 0) ? aL : 0.0) + ((tg < Tt - 1) ? aR : 0.0);
+            acc += __shfl_xor(acc, 1);
+            if constexpr (NPA == 4) acc += __shfl_xor(acc, 2);
+            if (pp == 0) gob(node)[D + k] = acc;
+        }
+    };
     auto ar_terms = [&](int node) {   // AR threads < NPA*D: QiPhi mu_left + PhiTQi mu_right
         if (at >= 0 && at < NPA * D) {
             const int k = at / NPA, pp = at % NPA;
@@ -831,6 +869,16 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         if (i >= 1) cov_flush(i - 1);   // staged by phase 3 of step i-1
         if (i + 1 < n) cov_prefetch(i + 1);
         // ---------------- phase 1 ----------------
+        // WK: node i+1's right-neighbour / old means and node i+2's old row load
+        // now and land in LDS at the end of phase 1, so phase 2 can start the AR
+        // terms before the worker partials arrive
+        float nx1 = 0.f, ol1 = 0.f, o21 = 0.f;
+        if constexpr (WK) {
+            if (has_next && tid >= 128 && tid < 128 + D) {
+                right_regs(i + 1, nx1, ol1);
+                if (i + 2 < n) o21 = xo[(size_t)(i + 2) * D + (tid - 128)];
+            }
+        }
         if (has_prev && tid < M2) {   // node i-1: statistics and slice (U,V) <- new
             const double vo = (double)orow(i - 1)[tid], vn = (double)mu_prev[2 + tid];
             ssq[tid] = ssq[tid] - vo * vo + vn * vn;
@@ -942,6 +990,13 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             if (wave == 1) P2STAMP(7);
             if (!WK && has_next) stage_z(i + 1, i);
             STAMPW(7, 0);
+        }
+        if constexpr (WK) {
+            if (has_next && tid >= 128 && tid < 128 + D) {
+                mu_right[tid - 128] = nx1;
+                mu_old_n[tid - 128] = ol1;
+                oring[((i + 2) & 3) * D + (tid - 128)] = o21;   // node i-2's slot: not read this step
+            }
         }
         // MG: node i-1's (U,V) row (stored by wave 0 in the previous step) is
         // read by this step's GEMV in waves 1-3: drain it before the barrier
@@ -1123,14 +1178,17 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             // waves 1-3: next-node loads first (latency hidden by the GEMV), GEMV, then hand-offs
             float nx = 0.f, ol = 0.f;
             float o2 = 0.f;
-            if (tid >= 128 && tid < 128 + D) {
+            if (!WK && tid >= 128 && tid < 128 + D) {
                 right_regs(i + 1, nx, ol);
                 if (i + 2 < n) o2 = xo[(size_t)(i + 2) * D + (tid - 128)];
             }
             uint64_t g0[KH];
             if (wave == 1) first_poll(i + 1, g0);
+            double aR = 0.0;
             if constexpr (WK) {
                 gather(i + 1);
+                aR = ar_right();   // mu_right landed in phase 1; after the gather, whose
+                                   // cross-CU loads set when waves 2-3 signal
             } else {
                 if (i + 2 < n) prefetch_y(i + 2);
                 gemv(tid - 64);
@@ -1142,7 +1200,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 else zero_left();
                 STAMPW(12, 64);
             }
-            if (tid >= 128 && tid < 128 + D) {
+            if (!WK && tid >= 128 && tid < 128 + D) {
                 mu_right[tid - 128] = nx;
                 mu_old_n[tid - 128] = ol;
                 oring[((i + 2) & 3) * D + (tid - 128)] = o2;   // node i-2's slot: not read this step
@@ -1155,7 +1213,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 ame::lds_wait_ge(wsync, 3u * (uint32_t)(i + 1), a.status, dead);
                 P2STAMP(6);
                 gemv_reduce(i + 1);
-                ar_terms(i + 1);
+                ar_left_finish(i + 1, aR);
                 P2STAMP(2 * (wave - 1) + 1);
             }
         }
