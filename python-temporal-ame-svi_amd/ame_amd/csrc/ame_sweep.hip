@@ -595,21 +595,35 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     // workers (fixed order),
     // plus row AME_GW = nodes node-3, node-2 (new means, LDS ring), and the raw
     // y_{node,node-1} for the Woodbury observation of the next step
+    // every load issued before any is checked: each is a cross-CU round trip.
+    // gather_issue(node) runs a phase ahead of gather(node) (phase 1 of the same
+    // step; the prologue for node 0): the workers publish partial m as soon as
+    // node m-4 is known, so the partials of node i+1 are normally in L2 by then
+    // and phase 2 mostly checks tags.  Every gather(node) must follow a
+    // gather_issue(node): the entries past the partials are pre-tagged there.
+    constexpr int GNE = AME_GW * PW, GGE = (GNE + 127) / 128;
+    uint64_t gv[GGE];
+    auto gather_issue = [&](int node) {
+        const int ht = tid - 128;
+        if (ht < 0) return;
+        const uint32_t want = ((a.epoch & 0xFFFFu) << 16) | ((uint32_t)node & 0xFFFFu);
+        const uint64_t* hp = (const uint64_t*)a.work + (size_t)tl * AME_GW * AME_GW_RING * PW;
+        const uint64_t* hs = hp + (size_t)(node % AME_GW_RING) * PW;
+#pragma unroll
+        for (int u = 0; u < GGE; ++u) {
+            const int e = ht + 128 * u, g = e / PW, c = e - g * PW;
+            gv[u] = (e < GNE) ? gran_load_agent(hs + (size_t)g * AME_GW_RING * PW + c)
+                              : ((uint64_t)want << 32);
+        }
+    };
     auto gather = [&](int node) {
         const int ht = tid - 128;
         if (ht < 0) return;
         const uint32_t want = ((a.epoch & 0xFFFFu) << 16) | ((uint32_t)node & 0xFFFFu);
         const uint64_t* hp = (const uint64_t*)a.work + (size_t)tl * AME_GW * AME_GW_RING * PW;
-        // every load issued before any is checked: each is a cross-CU round trip
-        constexpr int NE = AME_GW * PW, GE = (NE + 127) / 128;
+        constexpr int NE = GNE, GE = GGE;
         const uint64_t* hs = hp + (size_t)(node % AME_GW_RING) * PW;
-        uint64_t v[GE];
-#pragma unroll
-        for (int u = 0; u < GE; ++u) {
-            const int e = ht + 128 * u, g = e / PW, c = e - g * PW;
-            v[u] = (e < NE) ? gran_load_agent(hs + (size_t)g * AME_GW_RING * PW + c)
-                            : ((uint64_t)want << 32);
-        }
+        uint64_t (&v)[GE] = gv;   // issued by gather_issue(node)
         bool ok = true;
 #pragma unroll
         for (int u = 0; u < GE; ++u) ok = ok && (uint32_t)(v[u] >> 32) == want;
@@ -848,7 +862,10 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     if (!WK && n > 1) prefetch_y(1);
     __syncthreads();
     if (wave >= 1) {
-        if constexpr (WK) gather(0);   // waves 2-3
+        if constexpr (WK) {   // waves 2-3
+            gather_issue(0);
+            gather(0);
+        }
         else gemv(tid - 64);
     }
     __syncthreads();
@@ -874,6 +891,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         // terms before the worker partials arrive
         float nx1 = 0.f, ol1 = 0.f, o21 = 0.f;
         if constexpr (WK) {
+            if (has_next) gather_issue(i + 1);
             if (has_next && tid >= 128 && tid < 128 + D) {
                 right_regs(i + 1, nx1, ol1);
                 if (i + 2 < n) o21 = xo[(size_t)(i + 2) * D + (tid - 128)];
