@@ -1240,12 +1240,34 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         STAMP(2);
         // ---------------- phase 3 ----------------
         {
+            // the LDS reads of QB rounds first, then their stores: a round's K / cst
+            // stores otherwise keep the next round's reads behind them (the compiler
+            // cannot tell the addresses apart), serialising the rounds.  Each
+            // thread owns its (k, m) entries, and only k >= m is read.
+            constexpr int QB = 3;
 #pragma unroll
-            for (int qq = 0; qq < LTQ; ++qq) {
+            for (int q0 = 0; q0 < LTQ; q0 += QB) {
+            double kr[QB], u0[QB], u1[QB], u2[QB], u3[QB], u4[QB], u5[QB], u6[QB], u7[QB];
+            float ckm[QB], cmk[QB];
+#pragma unroll
+            for (int b = 0; b < QB; ++b) {
+                const int qq = q0 + b;
+                const bool ok = qq < LTQ && lk[qq < LTQ ? qq : 0] >= 0;
+                const int k = ok ? lk[qq] : 0, m = ok ? lm[qq] : 0;
+                kr[b] = K[k * KS + m];
+                u0[b] = upd[k]; u1[b] = upd[2 * D + m]; u2[b] = upd[D + k]; u3[b] = upd[3 * D + m];
+                u4[b] = upd[4 * D + k]; u5[b] = upd[6 * D + m]; u6[b] = upd[5 * D + k]; u7[b] = upd[7 * D + m];
+                ckm[b] = cob[k * D + m];
+                cmk[b] = cob[m * D + k];
+            }
+#pragma unroll
+            for (int b = 0; b < QB; ++b) {
+                const int qq = q0 + b;
+                if (qq >= LTQ) continue;
                 const int k = lk[qq], m = lm[qq];
                 if (k < 0) continue;
-                const double c = K[k * KS + m] - (upd[k] * upd[2 * D + m] + upd[D + k] * upd[3 * D + m]);
-                const double kn = c + (upd[4 * D + k] * upd[6 * D + m] + upd[5 * D + k] * upd[7 * D + m]);
+                const double c = kr[b] - (u0[b] * u1[b] + u2[b] * u3[b]);
+                const double kn = c + (u4[b] * u5[b] + u6[b] * u7[b]);
                 K[k * KS + m] = kn;
                 K[m * KS + k] = kn;
                 float c32;
@@ -1256,8 +1278,9 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                     if (is_bad && ((k < 2) != (m < 2))) c32 = 0.f;
                     if (k == m) c32 = c32 + 1e-6f;
                 }
-                cst[k * D + m] = __fadd_rn(__fmul_rn(lr, c32), __fmul_rn(om, cob[k * D + m]));
-                if (k != m) cst[m * D + k] = __fadd_rn(__fmul_rn(lr, c32), __fmul_rn(om, cob[m * D + k]));
+                cst[k * D + m] = __fadd_rn(__fmul_rn(lr, c32), __fmul_rn(om, ckm[b]));
+                if (k != m) cst[m * D + k] = __fadd_rn(__fmul_rn(lr, c32), __fmul_rn(om, cmk[b]));
+            }
             }
             STAMPW(14, 0);
             if (!WK && has_next) {
