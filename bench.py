@@ -171,16 +171,12 @@ def isolated_ms(eng, reps=5):
         eng.launch_elbo()
         torch.cuda.synchronize(eng.dev)
     ms, _ = eng.kernel_ms()
-    # the pair kernel alone (AME_ELBO_PAIRS_ONLY: ame_elbo launches only it)
+    # the pair kernel alone (diagnostic entry point ame_elbo_pairs_diag)
     eng.events.clear()
-    os.environ["AME_ELBO_PAIRS_ONLY"] = "1"
-    try:
-        for _ in range(reps):
-            eng.launch_elbo()
-            torch.cuda.synchronize(eng.dev)
-        ms["pairs"] = eng.kernel_ms()[0].get("elbo")
-    finally:
-        del os.environ["AME_ELBO_PAIRS_ONLY"]
+    for _ in range(reps):
+        eng.launch_elbo(pairs_only=True)
+        torch.cuda.synchronize(eng.dev)
+    ms["pairs"] = eng.kernel_ms()[0].get("pairs")
     eng.timing = False
     eng.invalidate()
     return ms

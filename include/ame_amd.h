@@ -57,6 +57,32 @@ enum ame_variant { AME_GOOD = 0, AME_BAD = 1, AME_NAIVE = 2 };
 /* float offset of the done word in a back channel of n*d floats */
 #define AME_BACK_DONE_OFFSET(nd) ((((nd) + 63) / 64) * 64)
 
+/* Sweep kernels.  Concrete kinds (what ame_sweep launches):
+ *   AME_SWEEP_V3          one 512-thread workgroup per slice (solver wave + 7
+ *                         helper waves, slice (U,V) in registers/LDS); d <= 64
+ *   AME_SWEEP_V2_LDS      one 256-thread workgroup per slice, (U,V) block in LDS
+ *   AME_SWEEP_V2_HBM      same, (U,V) block in HBM (args.work)
+ *   AME_SWEEP_V2_WORKERS  v2 plus seven GEMV worker workgroups per slice holding
+ *                         the (U,V) block in registers (partial ring in args.work)
+ * Requests (resolved by ame_sweep_kind for given dims):
+ *   AME_SWEEP_AUTO        V3 when the shape fits it, else AME_SWEEP_V2_AUTO
+ *   AME_SWEEP_V2_AUTO     V2_WORKERS when their workgroups are co-resident, else
+ *                         AME_SWEEP_V2_SINGLE
+ *   AME_SWEEP_V2_SINGLE   V2_LDS when the block fits one CU's LDS, else V2_HBM
+ * A concrete kind is also a valid request (resolved to itself or rejected). */
+enum ame_sweep_kind_code {
+    AME_SWEEP_AUTO = 0,
+    AME_SWEEP_V2_SINGLE = 1,
+    AME_SWEEP_V2_AUTO = 2,
+    AME_SWEEP_V3 = 3,
+    AME_SWEEP_V2_LDS = 20,
+    AME_SWEEP_V2_HBM = 21,
+    AME_SWEEP_V2_WORKERS = 22
+};
+
+/* ELBO pair kernels (ame_elbo_args.pairs_kernel): AUTO = V2 (LDS-DMA rows). */
+enum ame_pairs_kernel_code { AME_PAIRS_AUTO = 0, AME_PAIRS_V1 = 1, AME_PAIRS_V2 = 2 };
+
 typedef struct ame_dims {
     int32_t n;        /* nodes */
     int32_t r;        /* latent_dim; d = 2 + 2r */
@@ -104,6 +130,12 @@ typedef struct ame_sweep_args {
                                     slice fills with its new means when it finishes, or NULL */
     const float* back_in;        /* the right neighbour's back_out: in a pipelined launch
                                     (wait_epoch != 0) it replaces next_old */
+    int32_t kind;                /* enum ame_sweep_kind_code: the kernel the caller sized the
+                                    buffers for (normally the concrete kind ame_sweep_kind
+                                    returned); a request it does not resolve to is rejected */
+    uint32_t pad_;               /* zero */
+    uint64_t work_doubles;       /* size of `work` in doubles, checked against
+                                    ame_sweep_work_size(dims, kind) */
 } ame_sweep_args;
 
 typedef struct ame_cov_args {
@@ -123,6 +155,7 @@ typedef struct ame_elbo_args {
     int32_t swap_consistent;     /* 1: Y[j][i] == swap(Y[i][j]) for all pairs (checked at pack) */
     double* work;                /* scratch, >= ame_elbo_work_size() doubles */
     double* out;                 /* [8] sufficient sums (see ame_elbo doc) */
+    int32_t pairs_kernel;        /* enum ame_pairs_kernel_code (0 = default) */
 } ame_elbo_args;
 
 /* Relayout Y [n][n][T_total][2] -> Yt [T_local][n][n][2] for slices
@@ -138,25 +171,27 @@ int ame_pack_y(const float* Y, float* Yt, const ame_dims* dims,
  * and of node i at t-1, and old means of nodes j>i at t and of node i at t+1. */
 int ame_sweep(const ame_dims* dims, const ame_sweep_args* args, void* stream);
 
-/* 1 when ame_sweep for (n, r) honours done / wait_epoch, else 0. */
-int ame_sweep_orders_slices(int n, int r);
+/* 1 when the sweep kernel `kind` (concrete) honours done / wait_epoch, else 0. */
+int ame_sweep_orders_slices(int n, int r, int kind);
 
-/* Which sweep kernel ame_sweep launches for these dims (diagnostics, tests):
- * 4 / 3 = the v4 / v3 single-workgroup-per-slice kernels; 22 = v2 with seven
- * GEMV worker workgroups per slice (the slice's (U,V) block in their
- * registers); 21 = v2 with the block in HBM; 20 = v2 with it in LDS;
- * -1 = unsupported dims. */
-int ame_sweep_kind(const ame_dims* dims);
+/* The concrete kernel (enum ame_sweep_kind_code) a request resolves to for
+ * these dims, or -1 (unsupported dims, or the requested kernel cannot run
+ * them; see ame_last_error).  Nothing in the library reads the environment:
+ * the kind is chosen here, by the caller's request, once. */
+int ame_sweep_kind(const ame_dims* dims, int request);
 
-/* Scratch doubles ame_sweep needs in args->work (see the field). */
-long long ame_sweep_work_size(const ame_dims* dims);
+/* Scratch doubles ame_sweep needs in args->work for a concrete kind (see the
+ * field); -1 on bad dims / kind. */
+long long ame_sweep_work_size(const ame_dims* dims, int kind);
 
-/* Largest T_local ame_sweep can run with for (n, r) on this device, 0 if the
- * per-slice state does not fit one workgroup. */
-int ame_sweep_max_slices(int n, int r);
+/* Largest T_local one ame_sweep launch can hold for (n, r) and a request on
+ * this device (all its workgroups co-resident), 0 if the per-slice state does
+ * not fit.  For AME_SWEEP_AUTO / V2_AUTO with v2 this counts the slice
+ * workgroups alone (workers are then used when they fit, ame_sweep_kind). */
+int ame_sweep_max_slices(int n, int r, int request);
 
-/* Dynamic LDS bytes ame_sweep needs per workgroup (0 = unsupported r). */
-long long ame_sweep_lds_bytes(int n, int r);
+/* Dynamic LDS bytes per slice workgroup of a concrete kind (0 = unsupported). */
+long long ame_sweep_lds_bytes(int n, int r, int kind);
 
 /* Per-(node, local slice) covariance terms of the ELBO (log|S|, tr S,
  * tr(Qinv S), tr(S0inv S)), fully parallel: 64/(2r) covariances per wave. */
@@ -172,6 +207,11 @@ int ame_elbo(const ame_dims* dims, const ame_elbo_args* args, void* stream);
 
 /* Scratch doubles ame_elbo needs. */
 long long ame_elbo_work_size(const ame_dims* dims);
+
+/* Diagnostic (timing) entry point: launches ONLY the pair kernel of ame_elbo
+ * (its per-workgroup partials land in args->work; args->out is NOT written).
+ * Not part of an iteration; bench.py times the pair kernel alone with it. */
+int ame_elbo_pairs_diag(const ame_dims* dims, const ame_elbo_args* args, void* stream);
 
 /* Pin + map host memory for device access; *dev receives the device address
  * (utility; the multi-GPU path uses the peer buffers below). */

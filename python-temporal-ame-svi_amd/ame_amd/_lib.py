@@ -17,6 +17,11 @@ AME_STATUS_SPIN_TIMEOUT = 1
 AME_STATUS_HALO_TIMEOUT = 2
 AME_STATUS_LDS_TIMEOUT = 4
 AME_PEER_HANDLE_BYTES = 64
+# sweep kernel requests / kinds (enum ame_sweep_kind_code)
+AME_SWEEP_AUTO, AME_SWEEP_V2_SINGLE, AME_SWEEP_V2_AUTO, AME_SWEEP_V3 = 0, 1, 2, 3
+AME_SWEEP_V2_LDS, AME_SWEEP_V2_HBM, AME_SWEEP_V2_WORKERS = 20, 21, 22
+# ELBO pair kernels (enum ame_pairs_kernel_code)
+AME_PAIRS_AUTO, AME_PAIRS_V1, AME_PAIRS_V2 = 0, 1, 2
 
 c_int32 = ctypes.c_int32
 c_vp = ctypes.c_void_p
@@ -33,7 +38,8 @@ class ame_sweep_args(ctypes.Structure):
                 ("consts", c_vp), ("rinv", ctypes.c_double * 4), ("lr", ctypes.c_float),
                 ("one_minus_lr", ctypes.c_float), ("epoch", ctypes.c_uint32), ("status", c_vp),
                 ("work", c_vp), ("cov_new", c_vp), ("done", c_vp),
-                ("wait_epoch", ctypes.c_uint32), ("back_out", c_vp), ("back_in", c_vp)]
+                ("wait_epoch", ctypes.c_uint32), ("back_out", c_vp), ("back_in", c_vp),
+                ("kind", c_int32), ("pad_", ctypes.c_uint32), ("work_doubles", ctypes.c_uint64)]
 
 
 class ame_cov_args(ctypes.Structure):
@@ -43,12 +49,13 @@ class ame_cov_args(ctypes.Structure):
 class ame_elbo_args(ctypes.Structure):
     _fields_ = [("Yt", c_vp), ("x", c_vp), ("prev_final", c_vp), ("cov_terms", c_vp),
                 ("consts", c_vp), ("phi", c_vp), ("rinv", ctypes.c_double * 4),
-                ("swap_consistent", c_int32), ("work", c_vp), ("out", c_vp)]
+                ("swap_consistent", c_int32), ("work", c_vp), ("out", c_vp),
+                ("pairs_kernel", c_int32)]
 
 
 # every symbol include/ame_amd.h declares (checked by tests/test_capi.py)
 EXPORTS = ("ame_pack_y", "ame_sweep", "ame_sweep_kind", "ame_sweep_work_size", "ame_sweep_orders_slices", "ame_sweep_max_slices", "ame_sweep_lds_bytes", "ame_cov",
-           "ame_elbo", "ame_elbo_work_size", "ame_host_register", "ame_host_unregister",
+           "ame_elbo", "ame_elbo_work_size", "ame_elbo_pairs_diag", "ame_host_register", "ame_host_unregister",
            "ame_peer_alloc", "ame_peer_free", "ame_peer_open", "ame_peer_close",
            "ame_supported_r", "ame_last_error", "ame_version", "ame_align_work_size",
            "ame_align_cross_size", "ame_align_partials_size", "ame_align_cross", "ame_align_apply")
@@ -61,20 +68,24 @@ def _declare(L):
     P = ctypes.POINTER
     L.ame_pack_y.argtypes = [c_vp, c_vp, P(ame_dims), c_vp, c_vp]
     L.ame_sweep.argtypes = [P(ame_dims), P(ame_sweep_args), c_vp]
-    L.ame_sweep_max_slices.argtypes = [ctypes.c_int, ctypes.c_int]
-    L.ame_sweep_lds_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
+    L.ame_sweep_max_slices.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    L.ame_sweep_lds_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
     L.ame_sweep_lds_bytes.restype = ctypes.c_longlong
     L.ame_cov.argtypes = [P(ame_dims), P(ame_cov_args), c_vp]
     L.ame_elbo.argtypes = [P(ame_dims), P(ame_elbo_args), c_vp]
+    L.ame_elbo_pairs_diag.argtypes = [P(ame_dims), P(ame_elbo_args), c_vp]
+    L.ame_elbo_pairs_diag.restype = ctypes.c_int
+    L.ame_debug_gw_tag.argtypes = [ctypes.c_uint, ctypes.c_int]
+    L.ame_debug_gw_tag.restype = ctypes.c_uint
     L.ame_elbo_work_size.argtypes = [P(ame_dims)]
     L.ame_elbo_work_size.restype = ctypes.c_longlong
     L.ame_debug_selftest.argtypes = [c_vp, c_vp]
     L.ame_debug_selftest.restype = ctypes.c_int
-    L.ame_sweep_orders_slices.argtypes = [ctypes.c_int, ctypes.c_int]
+    L.ame_sweep_orders_slices.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
     L.ame_sweep_orders_slices.restype = ctypes.c_int
-    L.ame_sweep_kind.argtypes = [P(ame_dims)]
+    L.ame_sweep_kind.argtypes = [P(ame_dims), ctypes.c_int]
     L.ame_sweep_kind.restype = ctypes.c_int
-    L.ame_sweep_work_size.argtypes = [P(ame_dims)]
+    L.ame_sweep_work_size.argtypes = [P(ame_dims), ctypes.c_int]
     L.ame_sweep_work_size.restype = ctypes.c_longlong
     L.ame_supported_r.argtypes = [P(ctypes.c_int), ctypes.c_int]
     L.ame_host_register.argtypes = [c_vp, ctypes.c_ulonglong, P(c_vp)]

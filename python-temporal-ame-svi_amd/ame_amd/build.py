@@ -13,8 +13,10 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libame_amd.so")
-SOURCES = ("ame_sweep.hip", "ame_sweep3.hip", "ame_sweep4.hip", "ame_cov.hip", "ame_elbo.hip", "ame_capi.hip",
+SOURCES = ("ame_sweep.hip", "ame_sweep3.hip", "ame_cov.hip", "ame_elbo.hip", "ame_capi.hip",
            "ame_selftest.hip", "ame_align.hip", "ame_parts.hip")
+# one-latent-dim diagnostic builds (-DAME_ONLY_R, tools/): no split parts, no router
+UNSPLIT_SOURCES = tuple(s for s in SOURCES if s != "ame_parts.hip")
 # Every latent dim 1..32 is compiled in; the heaviest sources are split into
 # parts by r % parts (ame_common.h AME_R_PART) so the build runs in parallel.
 SPLIT = {"ame_sweep.hip": 3, "ame_sweep3.hip": 2, "ame_elbo.hip": 2}

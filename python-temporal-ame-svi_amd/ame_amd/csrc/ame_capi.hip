@@ -2,24 +2,20 @@
 // Argument validation lives here so a bad call fails loudly with a message
 // instead of faulting on the GPU.
 #include <stdio.h>
-#include <stdlib.h>
 #include <string.h>
 
 #include "ame_common.h"
 
 int ame_sweep_dispatch(const ame_dims*, const ame_sweep_args*, hipStream_t);
-int ame_sweep_blocks_per_cu(int n, int r);
-long long ame_sweep_v2w_doubles(const ame_dims* dm);
+int ame_sweep_blocks_per_cu(int n, int r, int mode);
+int ame_sweep_workers_fit(const ame_dims* dm);
 int ame_sweep3_dispatch(const ame_dims*, const ame_sweep_args*, hipStream_t);
 int ame_sweep3_supported(int n, int r);
 int ame_sweep3_blocks_per_cu(int n, int r);
 long long ame_sweep3_work_doubles(const ame_dims*);
-int ame_sweep4_dispatch(const ame_dims*, const ame_sweep_args*, hipStream_t);
-int ame_sweep4_supported(int n, int r);
-int ame_sweep4_blocks_per_cu(int n, int r);
-long long ame_sweep4_work_doubles(const ame_dims*);
+int ame_sweep3_lds(int n, int r);
 int ame_cov_dispatch(const ame_dims*, const ame_cov_args*, hipStream_t);
-int ame_elbo_dispatch(const ame_dims*, const ame_elbo_args*, hipStream_t);
+int ame_elbo_dispatch(const ame_dims*, const ame_elbo_args*, hipStream_t, int pairs_only);
 long long ame_elbo_work_doubles(const ame_dims*);
 int ame_align_cross_dispatch(const float*, const float*, int, int, int, int, double*, double*,
                              hipStream_t);
@@ -45,25 +41,6 @@ static bool r_supported(int r) {
     }
 }
 
-static bool env_on(const char* name) {
-    const char* e = getenv(name);
-    return e && e[0] && e[0] != '0';
-}
-// v3 (solver + helper waves, register-resident slice GEMV) when the slice fits
-// its register budget, else v2.  v4 (the observation term on MFMA block GEMMs
-// plus a window GEMV, r <= 16, n % 4 == 0, n <= 2048) is opt-in with
-// AME_SWEEP_V4=1: it is exact (tests/test_gpu_sweep4.py) but its step period
-// measured longer than v3's (profiles/r02_v4_*).  AME_SWEEP_V2=1
-// forces the v2 kernel (A/B runs, tests).
-static bool use_v4(int n, int r) {
-    if (env_on("AME_SWEEP_V2") || !env_on("AME_SWEEP_V4")) return false;
-    return ame_sweep4_supported(n, r) != 0;
-}
-static bool use_v3(int n, int r) {
-    if (env_on("AME_SWEEP_V2")) return false;
-    return use_v4(n, r) || ame_sweep3_supported(n, r) != 0;
-}
-
 static int check_dims(const ame_dims* d) {
     if (d == nullptr) return fail("ame: dims is NULL");
     if (d->n < 2) return fail("ame: n must be >= 2 (got %d)", d->n);
@@ -87,7 +64,10 @@ extern "C" {
 
 const char* ame_last_error(void) { return g_err; }
 
-const char* ame_version(void) { return "ame_amd 0.1 gfx950"; }
+const char* ame_version(void) { return "ame_amd 0.3 gfx950"; }
+
+// test hook (not in the header): the GEMV-worker partial tag (ame_common.h)
+unsigned int ame_debug_gw_tag(unsigned int epoch, int m) { return ame_gw_tag(epoch, m); }
 
 int ame_supported_r(int* out, int cap) {
     int c = 0;
@@ -155,47 +135,106 @@ int ame_peer_close(void* dev) {
     return hipIpcCloseMemHandle(dev) == hipSuccess ? 0 : fail("ame_peer_close failed");
 }
 
-long long ame_sweep_lds_bytes(int n, int r) {
-    if (!r_supported(r) || n < 1) return 0;
-    return sweep_lds_layout(n, r, ame_sweep_force_global()).total;
-}
-
-int ame_sweep_max_slices(int n, int r) {
-    if (!r_supported(r)) return 0;
-    const bool v3 = use_v3(n, r);
-    if (!v3 && sweep_lds_layout(n, r, ame_sweep_force_global()).total > AME_LDS_MAX) return 0;
+static int device_cus() {
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    const int per_cu = use_v4(n, r) ? ame_sweep4_blocks_per_cu(n, r)
-                       : v3 ? ame_sweep3_blocks_per_cu(n, r) : ame_sweep_blocks_per_cu(n, r);
-    return per_cu * cus;
+    return cus;
 }
 
-int ame_sweep_orders_slices(int n, int r) { return r_supported(r) && use_v3(n, r) ? 1 : 0; }
-
-// v2 with GEMV workers: their partial ring; else v2 with the slice's (U,V)
-// block in HBM: [T_local][n][2r] fp32 in the work buffer
-static long long v2_global_doubles(const ame_dims* d) {
-    if (use_v3(d->n, d->r)) return 0;
-    if (const long long w = ame_sweep_v2w_doubles(d)) return w;
-    if (!sweep_lds_layout(d->n, d->r, ame_sweep_force_global()).m_global) return 0;
-    return ((long long)d->T_local * d->n * 2 * d->r + 1) / 2;
+static bool v2_block_in_lds(int n, int r) { return !sweep_lds_layout(n, r, 0).m_global; }
+static bool v2_single_fits(int n, int r) { return sweep_lds_layout(n, r, 1).total <= AME_LDS_MAX; }
+static bool is_concrete(int k) {
+    return k == AME_SWEEP_V3 || k == AME_SWEEP_V2_LDS || k == AME_SWEEP_V2_HBM || k == AME_SWEEP_V2_WORKERS;
 }
 
-int ame_sweep_kind(const ame_dims* dims) {
+// Request -> concrete kernel for these dims (-1 + message when it cannot run).
+// The choice depends only on the request and the shape: nothing reads the
+// environment, so a caller that sized its buffers for a kind gets that kind.
+static int resolve_kind(const ame_dims* d, int request) {
+    const int n = d->n, r = d->r;
+    switch (request) {
+        case AME_SWEEP_AUTO:
+            if (ame_sweep3_supported(n, r)) return AME_SWEEP_V3;
+            // fall through
+        case AME_SWEEP_V2_AUTO:
+            if (ame_sweep_workers_fit(d)) return AME_SWEEP_V2_WORKERS;
+            // fall through
+        case AME_SWEEP_V2_SINGLE:
+            if (v2_block_in_lds(n, r)) return AME_SWEEP_V2_LDS;
+            if (v2_single_fits(n, r)) return AME_SWEEP_V2_HBM;
+            return fail("ame_sweep: no sweep kernel fits n=%d, r=%d", n, r);
+        case AME_SWEEP_V3:
+            if (ame_sweep3_supported(n, r)) return AME_SWEEP_V3;
+            return fail("ame_sweep: the v3 sweep does not fit n=%d, r=%d", n, r);
+        case AME_SWEEP_V2_LDS:
+            if (v2_block_in_lds(n, r)) return AME_SWEEP_V2_LDS;
+            return fail("ame_sweep: the (U,V) block of n=%d, r=%d does not fit in LDS", n, r);
+        case AME_SWEEP_V2_HBM:
+            if (v2_single_fits(n, r)) return AME_SWEEP_V2_HBM;
+            return fail("ame_sweep: the v2 sweep does not fit n=%d, r=%d", n, r);
+        case AME_SWEEP_V2_WORKERS:
+            if (ame_sweep_workers_fit(d)) return AME_SWEEP_V2_WORKERS;
+            return fail("ame_sweep: GEMV workers do not fit n=%d, T_local=%d", n, d->T_local);
+        default:
+            return fail("ame_sweep: unknown sweep kind request %d", request);
+    }
+}
+
+long long ame_sweep_lds_bytes(int n, int r, int kind) {
+    if (!r_supported(r) || n < 1) return 0;
+    switch (kind) {
+        case AME_SWEEP_V3: return ame_sweep3_supported(n, r) ? ame_sweep3_lds(n, r) : 0;
+        case AME_SWEEP_V2_LDS: return ame_v2_mode_lds(n, r, 0);
+        case AME_SWEEP_V2_HBM: return ame_v2_mode_lds(n, r, 1);
+        case AME_SWEEP_V2_WORKERS: return ame_v2_mode_lds(n, r, 2);
+        default: return 0;
+    }
+}
+
+int ame_sweep_max_slices(int n, int r, int request) {
+    if (!r_supported(r) || n < 2) return 0;
+    const int cus = device_cus();
+    switch (request) {
+        case AME_SWEEP_AUTO:
+            if (ame_sweep3_supported(n, r)) return ame_sweep3_blocks_per_cu(n, r) * cus;
+            // fall through
+        case AME_SWEEP_V2_AUTO:
+        case AME_SWEEP_V2_SINGLE:
+            if (v2_block_in_lds(n, r)) return ame_sweep_blocks_per_cu(n, r, 0) * cus;
+            return v2_single_fits(n, r) ? ame_sweep_blocks_per_cu(n, r, 1) * cus : 0;
+        case AME_SWEEP_V3:
+            return ame_sweep3_supported(n, r) ? ame_sweep3_blocks_per_cu(n, r) * cus : 0;
+        case AME_SWEEP_V2_LDS:
+            return v2_block_in_lds(n, r) ? ame_sweep_blocks_per_cu(n, r, 0) * cus : 0;
+        case AME_SWEEP_V2_HBM:
+            return v2_single_fits(n, r) ? ame_sweep_blocks_per_cu(n, r, 1) * cus : 0;
+        case AME_SWEEP_V2_WORKERS:
+            return ame_sweep_blocks_per_cu(n, r, 2) * cus / (1 + AME_GW);
+        default:
+            return 0;
+    }
+}
+
+int ame_sweep_orders_slices(int n, int r, int kind) {
+    return r_supported(r) && kind == AME_SWEEP_V3 && ame_sweep3_supported(n, r) ? 1 : 0;
+}
+
+int ame_sweep_kind(const ame_dims* dims, int request) {
     if (check_dims(dims)) return -1;
-    if (use_v4(dims->n, dims->r)) return 4;
-    if (use_v3(dims->n, dims->r)) return 3;
-    if (ame_sweep_v2w_doubles(dims) > 0) return 22;
-    return sweep_lds_layout(dims->n, dims->r, ame_sweep_force_global()).m_global ? 21 : 20;
+    return resolve_kind(dims, request);
 }
 
-long long ame_sweep_work_size(const ame_dims* dims) {
+long long ame_sweep_work_size(const ame_dims* dims, int kind) {
     if (check_dims(dims)) return -1;
-    if (use_v4(dims->n, dims->r)) return ame_sweep4_work_doubles(dims);
-    const long long a = ame_sweep3_work_doubles(dims), b = v2_global_doubles(dims);
-    return a > b ? a : b;
+    switch (kind) {
+        case AME_SWEEP_V3: return ame_sweep3_work_doubles(dims);
+        case AME_SWEEP_V2_LDS: return 0;
+        // [T_local][n][2r] fp32 (U,V) copy
+        case AME_SWEEP_V2_HBM: return ((long long)dims->T_local * dims->n * 2 * dims->r + 1) / 2;
+        case AME_SWEEP_V2_WORKERS: return ame_v2_ring_doubles(dims);
+        default: return fail("ame_sweep_work_size: %d is not a concrete sweep kind", kind);
+    }
 }
 
 int ame_pack_y(const float* Y, float* Yt, const ame_dims* dims, unsigned long long* mismatch,
@@ -214,19 +253,23 @@ int ame_sweep(const ame_dims* dims, const ame_sweep_args* a, void* stream) {
         return fail("ame_sweep: t_begin=%d > 0 needs halo_in", dims->t_begin);
     if (dims->t_begin + dims->T_local < dims->T_total && !a->next_old && !(a->wait_epoch && a->back_in))
         return fail("ame_sweep: rank does not hold T-1 and next_old is NULL");
-    const bool v3 = use_v3(dims->n, dims->r);
-    if (!v3 && sweep_lds_layout(dims->n, dims->r, ame_sweep_force_global()).total > AME_LDS_MAX)
-        return fail("ame_sweep: slice state (n=%d, r=%d) exceeds one workgroup's LDS", dims->n, dims->r);
-    if ((v2_global_doubles(dims) > 0 || use_v4(dims->n, dims->r)) && !a->work)
-        return fail("ame_sweep: n=%d, r=%d keeps the slice in HBM and needs the work buffer", dims->n, dims->r);
-    if (a->wait_epoch != 0 && (!v3 || !a->done))
-        return fail("ame_sweep: wait_epoch needs the v3 sweep and a done array");
-    const int maxs = ame_sweep_max_slices(dims->n, dims->r);
+    const int kind = resolve_kind(dims, a->kind);
+    if (kind < 0) return -1;
+    if (is_concrete(a->kind) && kind != a->kind)
+        return fail("ame_sweep: requested kind %d resolves to %d", a->kind, kind);
+    const long long need = ame_sweep_work_size(dims, kind);
+    if (need > 0 && (!a->work || a->work_doubles < (unsigned long long)need))
+        return fail("ame_sweep: the work buffer holds %d doubles, kind %d needs more", (int)a->work_doubles, kind);
+    if (a->wait_epoch != 0 && (!ame_sweep_orders_slices(dims->n, dims->r, kind) || !a->done))
+        return fail("ame_sweep: wait_epoch needs a kernel that orders slices (kind %d) and a done array", kind);
+    const int maxs = kind == AME_SWEEP_V2_WORKERS ? dims->T_local
+                                                   : ame_sweep_max_slices(dims->n, dims->r, kind);
     if (dims->T_local > maxs)
         return fail("ame_sweep: T_local=%d exceeds co-resident workgroups (%d)", dims->T_local, maxs);
-    if (use_v4(dims->n, dims->r)) return launched(ame_sweep4_dispatch(dims, a, (hipStream_t)stream), "sweep4");
-    if (v3) return launched(ame_sweep3_dispatch(dims, a, (hipStream_t)stream), "sweep3");
-    return launched(ame_sweep_dispatch(dims, a, (hipStream_t)stream), "sweep");
+    ame_sweep_args c = *a;
+    c.kind = kind;
+    if (kind == AME_SWEEP_V3) return launched(ame_sweep3_dispatch(dims, &c, (hipStream_t)stream), "sweep3");
+    return launched(ame_sweep_dispatch(dims, &c, (hipStream_t)stream), "sweep");
 }
 
 int ame_cov(const ame_dims* dims, const ame_cov_args* a, void* stream) {
@@ -246,7 +289,17 @@ int ame_elbo(const ame_dims* dims, const ame_elbo_args* a, void* stream) {
         return fail("ame_elbo: NULL buffer");
     if (dims->t_begin > 0 && !a->prev_final)
         return fail("ame_elbo: t_begin=%d > 0 needs prev_final", dims->t_begin);
-    return launched(ame_elbo_dispatch(dims, a, (hipStream_t)stream), "elbo");
+    if (a->pairs_kernel < AME_PAIRS_AUTO || a->pairs_kernel > AME_PAIRS_V2)
+        return fail("ame_elbo: bad pairs_kernel %d", a->pairs_kernel);
+    return launched(ame_elbo_dispatch(dims, a, (hipStream_t)stream, 0), "elbo");
+}
+
+int ame_elbo_pairs_diag(const ame_dims* dims, const ame_elbo_args* a, void* stream) {
+    if (int e = check_dims(dims)) return e;
+    if (!a || !a->Yt || !a->x || !a->work) return fail("ame_elbo_pairs_diag: NULL buffer");
+    if (a->pairs_kernel < AME_PAIRS_AUTO || a->pairs_kernel > AME_PAIRS_V2)
+        return fail("ame_elbo_pairs_diag: bad pairs_kernel %d", a->pairs_kernel);
+    return launched(ame_elbo_dispatch(dims, a, (hipStream_t)stream, 1), "elbo_pairs");
 }
 
 static int check_align(int n, int T, int r) {

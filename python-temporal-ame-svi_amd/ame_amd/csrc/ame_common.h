@@ -2,7 +2,6 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <stdlib.h>
 
 #include "../../../include/ame_amd.h"
 
@@ -101,12 +100,35 @@ __host__ __device__ inline SweepLds sweep_lds_layout(int n, int R, int force_glo
     return L;
 }
 
-// AME_SWEEP_M_GLOBAL=1 puts the v2 sweep's (U,V) block in HBM even when it
-// would fit in LDS (host side; lets the tests cover that mode at small n).
-inline int ame_sweep_force_global() {
-    const char* e = getenv("AME_SWEEP_M_GLOBAL");
-    return (e && e[0] && e[0] != '0') ? 1 : 0;
+// v2 sweep with GEMV workers (kind AME_SWEEP_V2_WORKERS, ame_sweep.hip)
+#define AME_GW 7          // GEMV worker workgroups per slice
+#define AME_GW_RING 8     // partial ring slots per worker
+#define AME_GW_MAXPW 152  // nodes per worker wave held in registers: n <= 7 * 4 * 152
+
+// Tag of worker partial m of sweep `epoch` in the partial ring.  Bit 31 is
+// always set, so a slot the launch zeroed can never match (an all-zero word
+// would otherwise equal node 0's tag whenever epoch % 2^15 == 0); 15 epoch
+// bits, 16 node bits (n <= 65535 when workers run).
+__host__ __device__ inline uint32_t ame_gw_tag(uint32_t epoch, int m) {
+    return 0x80000000u | ((epoch & 0x7FFFu) << 16) | ((uint32_t)m & 0xFFFFu);
 }
+
+// LDS of one v2 slice workgroup per mode (0: (U,V) in LDS, 1: in HBM, 2: workers)
+// and of a GEMV worker workgroup; a MODE 2 launch sizes for the larger
+__host__ __device__ inline long long ame_v2_worker_lds(int n, int R) {
+    const int NW = (n + AME_GW - 1) / AME_GW, ZN = 4 * AME_GW_MAXPW;
+    return ame_align16(8LL * (NW > ZN ? NW : ZN)) + 4LL * 4 * (2 * R + 2);
+}
+__host__ __device__ inline long long ame_v2_mode_lds(int n, int R, int mode) {
+    const long long m = sweep_lds_layout(n, R, mode != 0 ? 1 : 0).total;
+    if (mode != 2) return m;
+    const long long w = ame_v2_worker_lds(n, R);
+    return m > w ? m : w;
+}
+__host__ __device__ inline long long ame_v2_ring_doubles(const ame_dims* d) {
+    return (long long)d->T_local * AME_GW * AME_GW_RING * (2 * d->r + 2);
+}
+
 
 // Latent dims compiled into the library.  r = 32 (d = 66, BASELINE config 5)
 // runs on the v2 sweep only (two state rows per lane in the solver wave).

@@ -672,16 +672,15 @@ long long ame_elbo_work_doubles(const ame_dims* dm) {
 #endif
 
 template <int R>
-static int launch_elbo(const ame_dims* dm, const ame_elbo_args* a, hipStream_t st) {
+static int launch_elbo(const ame_dims* dm, const ame_elbo_args* a, hipStream_t st, bool pairs_only) {
     const long long b2 = pairs_blocks(dm, a->swap_consistent);
     const long long b3 = nodes_blocks(dm);
     double* p2 = a->work;
     double* p3 = a->work + 2 * b2;
     if (b2 > 0) {
         // LDS-DMA pair kernel when every Y row starts 16-byte aligned (n even);
-        // AME_PAIRS_V1=1 keeps the register-streaming kernel (A/B runs)
-        const char* e = getenv("AME_PAIRS_V1");
-        const bool v1 = (dm->n & 1) || (e && e[0] && e[0] != '0');
+        // args.pairs_kernel = AME_PAIRS_V1 keeps the register-streaming kernel
+        const bool v1 = (dm->n & 1) || a->pairs_kernel == AME_PAIRS_V1;
         if (v1)
             hipLaunchKernelGGL(ame_pairs_kernel<R>, dim3((unsigned)b2), dim3(AME_NT), 0, st, *dm, a->Yt,
                                a->x, a->rinv[0], a->rinv[1], a->rinv[2], a->rinv[3],
@@ -691,10 +690,8 @@ static int launch_elbo(const ame_dims* dm, const ame_elbo_args* a, hipStream_t s
                                a->x, a->rinv[0], a->rinv[1], a->rinv[2], a->rinv[3],
                                a->swap_consistent, p2);
     }
-    {   // timing knob (bench.py, tools): the pair kernel alone
-        const char* po = getenv("AME_ELBO_PAIRS_ONLY");
-        if (po && po[0] && po[0] != '0') return hipGetLastError() == hipSuccess ? 0 : -3;
-    }
+    if (pairs_only)   // ame_elbo_pairs_diag: timing of the pair kernel alone
+        return hipGetLastError() == hipSuccess ? 0 : -3;
     if (b3 > 0)
         hipLaunchKernelGGL(ame_nodes_kernel<R>, dim3((unsigned)b3), dim3(AME_NT), 0, st, *dm, a->x,
                            a->prev_final, a->cov_terms, a->consts, a->phi, p3);
@@ -703,10 +700,10 @@ static int launch_elbo(const ame_dims* dm, const ame_elbo_args* a, hipStream_t s
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-int AME_PFN(ame_elbo_dispatch)(const ame_dims* dm, const ame_elbo_args* a, hipStream_t st) {
+int AME_PFN(ame_elbo_dispatch)(const ame_dims* dm, const ame_elbo_args* a, hipStream_t st, int pairs_only) {
     switch (dm->r) {
 #define X(RR) \
-    case RR: return launch_elbo<RR>(dm, a, st);
+    case RR: return launch_elbo<RR>(dm, a, st, pairs_only != 0);
         AME_FOR_EACH_R(X)
 #undef X
         default: return -1;

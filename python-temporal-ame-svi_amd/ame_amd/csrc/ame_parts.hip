@@ -5,8 +5,8 @@
 
 #define AME_DECL_SWEEP(P)                                                                 \
     int ame_sweep_dispatch_p##P(const ame_dims*, const ame_sweep_args*, hipStream_t);     \
-    int ame_sweep_blocks_per_cu_p##P(int, int);                                           \
-    long long ame_sweep_v2w_doubles_p##P(const ame_dims*);
+    int ame_sweep_blocks_per_cu_p##P(int, int, int);                                      \
+    int ame_sweep_workers_fit_p##P(const ame_dims*);
 AME_DECL_SWEEP(0)
 AME_DECL_SWEEP(1)
 AME_DECL_SWEEP(2)
@@ -14,7 +14,8 @@ AME_DECL_SWEEP(2)
     int ame_sweep3_dispatch_p##P(const ame_dims*, const ame_sweep_args*, hipStream_t);    \
     int ame_sweep3_supported_p##P(int, int);                                              \
     int ame_sweep3_blocks_per_cu_p##P(int, int);                                          \
-    int ame_elbo_dispatch_p##P(const ame_dims*, const ame_elbo_args*, hipStream_t);
+    int ame_sweep3_lds_p##P(int, int);                                                    \
+    int ame_elbo_dispatch_p##P(const ame_dims*, const ame_elbo_args*, hipStream_t, int);
 AME_DECL_2(0)
 AME_DECL_2(1)
 
@@ -25,18 +26,18 @@ int ame_sweep_dispatch(const ame_dims* dm, const ame_sweep_args* a, hipStream_t 
         default: return ame_sweep_dispatch_p2(dm, a, st);
     }
 }
-int ame_sweep_blocks_per_cu(int n, int r) {
+int ame_sweep_blocks_per_cu(int n, int r, int mode) {
     switch (r % 3) {
-        case 0: return ame_sweep_blocks_per_cu_p0(n, r);
-        case 1: return ame_sweep_blocks_per_cu_p1(n, r);
-        default: return ame_sweep_blocks_per_cu_p2(n, r);
+        case 0: return ame_sweep_blocks_per_cu_p0(n, r, mode);
+        case 1: return ame_sweep_blocks_per_cu_p1(n, r, mode);
+        default: return ame_sweep_blocks_per_cu_p2(n, r, mode);
     }
 }
-long long ame_sweep_v2w_doubles(const ame_dims* dm) {
+int ame_sweep_workers_fit(const ame_dims* dm) {
     switch (dm->r % 3) {
-        case 0: return ame_sweep_v2w_doubles_p0(dm);
-        case 1: return ame_sweep_v2w_doubles_p1(dm);
-        default: return ame_sweep_v2w_doubles_p2(dm);
+        case 0: return ame_sweep_workers_fit_p0(dm);
+        case 1: return ame_sweep_workers_fit_p1(dm);
+        default: return ame_sweep_workers_fit_p2(dm);
     }
 }
 int ame_sweep3_dispatch(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {
@@ -48,6 +49,10 @@ int ame_sweep3_supported(int n, int r) {
 int ame_sweep3_blocks_per_cu(int n, int r) {
     return (r & 1) ? ame_sweep3_blocks_per_cu_p1(n, r) : ame_sweep3_blocks_per_cu_p0(n, r);
 }
-int ame_elbo_dispatch(const ame_dims* dm, const ame_elbo_args* a, hipStream_t st) {
-    return (dm->r & 1) ? ame_elbo_dispatch_p1(dm, a, st) : ame_elbo_dispatch_p0(dm, a, st);
+int ame_sweep3_lds(int n, int r) {
+    return (r & 1) ? ame_sweep3_lds_p1(n, r) : ame_sweep3_lds_p0(n, r);
+}
+int ame_elbo_dispatch(const ame_dims* dm, const ame_elbo_args* a, hipStream_t st, int pairs_only) {
+    return (dm->r & 1) ? ame_elbo_dispatch_p1(dm, a, st, pairs_only)
+                       : ame_elbo_dispatch_p0(dm, a, st, pairs_only);
 }

@@ -109,9 +109,7 @@ extern "C" int ame_debug_read_stamps(unsigned long long* host, int count) {
 #endif
 
 #define AME_YPF 8   // Y-row prefetch registers per thread (n <= 2048 fully prefetched)
-#define AME_GW 7          // GEMV workers per slice (MODE 2)
-#define AME_GW_RING 8     // partial ring slots per worker
-#define AME_GW_MAXPW 152  // nodes per worker wave held in registers: n <= 7 * 4 * 152
+// AME_GW, AME_GW_RING, AME_GW_MAXPW, ame_gw_tag: ame_common.h
 #ifndef AME_MG_UNROLL
 #define AME_MG_UNROLL 8   // GEMV rows in flight per thread when the slice is read from HBM
 #endif
@@ -177,7 +175,7 @@ __device__ __forceinline__ void tri_decode(int e, int& k, int& m) {
 // GEMV worker (MODE 2): workgroup TL + t*AME_GW + g owns nodes
 // [g*NW, (g+1)*NW) of slice t, NW = ceil(n / AME_GW); wave q holds nodes
 // base + q + 4s (s < AME_GW_MAXPW), lane c column c of (U,V), in registers.
-// Per node m it publishes (ring slot m % 8, tag = epoch16 << 16 | m16)
+// Per node m it publishes (ring slot m % 8, tag = ame_gw_tag(epoch, m))
 //   part[c'] = sum_{j in range, j not in [m-3, m]} z_mj . [V | U]_j   (c' < 2r)
 //   part[2r + p] = sum z_mj[p]
 // with node j's new mean for j <= m-4 (read from the slice's hand-off
@@ -201,7 +199,6 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
     uint64_t* hp = (uint64_t*)a.work + (size_t)(t * AME_GW + g) * AME_GW_RING * PW;
     const float* ysl = a.Yt + (size_t)t * n * n * 2;
     const float r00f = (float)a.rinv[0], r01f = (float)a.rinv[1], r10f = (float)a.rinv[2], r11f = (float)a.rinv[3];
-    const uint32_t etag = (a.epoch & 0xFFFFu) << 16;
     const bool col = lane < M2;
     bool dead = false;
     float mreg[AME_GW_MAXPW];
@@ -315,7 +312,7 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
         __syncthreads();
         if (tid < PW) {
             const float v = ((red[tid] + red[PW + tid]) + red[2 * PW + tid]) + red[3 * PW + tid];
-            const uint32_t tag = etag | ((uint32_t)m & 0xFFFFu);
+            const uint32_t tag = ame_gw_tag(a.epoch, m);
             gran_store_agent(hp + (size_t)(m % AME_GW_RING) * PW + tid,
                              ((uint64_t)tag << 32) | (uint64_t)__float_as_uint(v));
         }
@@ -606,7 +603,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     auto gather_issue = [&](int node) {
         const int ht = tid - 128;
         if (ht < 0) return;
-        const uint32_t want = ((a.epoch & 0xFFFFu) << 16) | ((uint32_t)node & 0xFFFFu);
+        const uint32_t want = ame_gw_tag(a.epoch, node);
         const uint64_t* hp = (const uint64_t*)a.work + (size_t)tl * AME_GW * AME_GW_RING * PW;
         const uint64_t* hs = hp + (size_t)(node % AME_GW_RING) * PW;
 #pragma unroll
@@ -619,7 +616,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     auto gather = [&](int node) {
         const int ht = tid - 128;
         if (ht < 0) return;
-        const uint32_t want = ((a.epoch & 0xFFFFu) << 16) | ((uint32_t)node & 0xFFFFu);
+        const uint32_t want = ame_gw_tag(a.epoch, node);
         const uint64_t* hp = (const uint64_t*)a.work + (size_t)tl * AME_GW * AME_GW_RING * PW;
         constexpr int NE = GNE, GE = GGE;
         const uint64_t* hs = hp + (size_t)(node % AME_GW_RING) * PW;
@@ -1298,20 +1295,9 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     cov_flush(n - 1);
 }
 
-static long long worker_lds(int n, int R) {
-    const int NW = (n + AME_GW - 1) / AME_GW, ZN = 4 * AME_GW_MAXPW;
-    return ame_align16(8LL * (NW > ZN ? NW : ZN)) + 4LL * 4 * (2 * R + 2);
-}
-static long long mode_lds(int n, int R, int mode) {
-    const long long m = sweep_lds_layout(n, R, mode != 0 ? 1 : 0).total;
-    if (mode != 2) return m;
-    const long long w = worker_lds(n, R);
-    return m > w ? m : w;
-}
-
 template <int R, int MODE>
 static int launch_sweep_t(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {
-    const long long lds = mode_lds(dm->n, R, MODE);
+    const long long lds = ame_v2_mode_lds(dm->n, R, MODE);
     auto kern = ame_sweep_kernel<R, MODE>;
     if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
         hipSuccess)
@@ -1319,8 +1305,8 @@ static int launch_sweep_t(const ame_dims* dm, const ame_sweep_args* a, hipStream
     int blocks = dm->T_local;
     if constexpr (MODE == 2) {
         blocks = dm->T_local * (1 + AME_GW);
-        // partial ring: no stale tag may match (tags carry the low 16 epoch bits)
-        const size_t bytes = (size_t)dm->T_local * AME_GW * AME_GW_RING * (2 * R + 2) * 8;
+        // partial ring: zero never matches a tag (ame_gw_tag sets bit 31)
+        const size_t bytes = (size_t)ame_v2_ring_doubles(dm) * 8;
         if (hipMemsetAsync(a->work, 0, bytes, st) != hipSuccess) return -3;
     }
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(AME_NT), (size_t)lds, st, *dm, *a);
@@ -1329,7 +1315,8 @@ static int launch_sweep_t(const ame_dims* dm, const ame_sweep_args* a, hipStream
 
 template <int R, int MODE>
 static int sweep_occupancy_t(int n) {
-    const long long lds = mode_lds(n, R, MODE);
+    const long long lds = ame_v2_mode_lds(n, R, MODE);
+    if (lds > AME_LDS_MAX) return 0;
     auto kern = ame_sweep_kernel<R, MODE>;
     if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
         hipSuccess)
@@ -1340,37 +1327,38 @@ static int sweep_occupancy_t(int n) {
     return per_cu;
 }
 
-static bool workers_env_off() {
-    const char* e = getenv("AME_SWEEP_NOWORKERS");
-    return e && e[0] && e[0] != '0';
-}
-
-// MODE 2 when its T_local * (1 + AME_GW) workgroups are co-resident and a
-// worker wave's node share fits its registers
+// MODE 2 can run when its T_local * (1 + AME_GW) workgroups are co-resident and
+// a worker wave's node share fits its registers
 template <int R>
-static bool use_workers(int n, int T_local) {
-    if (workers_env_off()) return false;
+static bool workers_fit(int n, int T_local) {
     const int NW = (n + AME_GW - 1) / AME_GW;
     if ((NW + 3) / 4 > AME_GW_MAXPW || n > 65535) return false;
-    if (mode_lds(n, R, 2) > AME_LDS_MAX) return false;
+    if (ame_v2_mode_lds(n, R, 2) > AME_LDS_MAX) return false;
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess) return false;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
     return (long long)T_local * (1 + AME_GW) <= (long long)sweep_occupancy_t<R, 2>(n) * cus;
 }
 
+// a->kind is concrete here (ame_capi.hip resolved and checked it)
 template <int R>
 static int launch_sweep(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {
-    if (use_workers<R>(dm->n, dm->T_local)) return launch_sweep_t<R, 2>(dm, a, st);
-    if (sweep_lds_layout(dm->n, R, ame_sweep_force_global()).m_global)
-        return launch_sweep_t<R, 1>(dm, a, st);
-    return launch_sweep_t<R, 0>(dm, a, st);
+    switch (a->kind) {
+        case AME_SWEEP_V2_WORKERS: return launch_sweep_t<R, 2>(dm, a, st);
+        case AME_SWEEP_V2_HBM: return launch_sweep_t<R, 1>(dm, a, st);
+        case AME_SWEEP_V2_LDS: return launch_sweep_t<R, 0>(dm, a, st);
+        default: return -1;
+    }
 }
 
 template <int R>
-static int sweep_occupancy(int n) {
-    if (sweep_lds_layout(n, R, ame_sweep_force_global()).m_global) return sweep_occupancy_t<R, 1>(n);
-    return sweep_occupancy_t<R, 0>(n);
+static int sweep_occupancy(int n, int mode) {
+    switch (mode) {
+        case 0: return sweep_occupancy_t<R, 0>(n);
+        case 1: return sweep_occupancy_t<R, 1>(n);
+        case 2: return sweep_occupancy_t<R, 2>(n);
+        default: return 0;
+    }
 }
 
 int AME_PFN(ame_sweep_dispatch)(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {
@@ -1383,21 +1371,22 @@ int AME_PFN(ame_sweep_dispatch)(const ame_dims* dm, const ame_sweep_args* a, hip
     }
 }
 
-int AME_PFN(ame_sweep_blocks_per_cu)(int n, int r) {
+// workgroups of one v2 launch per CU for a mode (0: block in LDS, 1: HBM, 2: workers)
+int AME_PFN(ame_sweep_blocks_per_cu)(int n, int r, int mode) {
     switch (r) {
 #define X(RR) \
-    case RR: return sweep_occupancy<RR>(n);
+    case RR: return sweep_occupancy<RR>(n, mode);
         AME_FOR_EACH_R(X)
 #undef X
         default: return 0;
     }
 }
 
-// v2 with GEMV workers: doubles of the partial ring in the work buffer (0 = not used)
-long long AME_PFN(ame_sweep_v2w_doubles)(const ame_dims* dm) {
+// 1 when the v2 sweep with GEMV workers can run these dims
+int AME_PFN(ame_sweep_workers_fit)(const ame_dims* dm) {
     switch (dm->r) {
 #define X(RR) \
-    case RR: return use_workers<RR>(dm->n, dm->T_local) ? (long long)dm->T_local * AME_GW * AME_GW_RING * (2 * RR + 2) : 0;
+    case RR: return workers_fit<RR>(dm->n, dm->T_local) ? 1 : 0;
         AME_FOR_EACH_R(X)
 #undef X
         default: return 0;

@@ -1137,6 +1137,16 @@ int AME_PFN(ame_sweep3_supported)(int n, int r) {
     }
 }
 
+int AME_PFN(ame_sweep3_lds)(int n, int r) {
+    switch (r) {
+#define X(RR) \
+    case RR: if constexpr (RR <= kV3MaxR) return l3_total<RR>(n); else return 0;
+        AME_FOR_EACH_R(X)
+#undef X
+        default: return 0;
+    }
+}
+
 template <int R>
 static int launch_sweep3(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {
     const int lds = l3_total<R>(dm->n);

@@ -134,9 +134,27 @@ class TimeShardHalo:
         dist.barrier(group=self.group)
         atexit.register(self.close)
 
-    def close(self):
+    def quiesce(self, eng):
+        """Called by every rank when fit() ends (after the dropped speculative
+        sweeps were queued behind): wait for this rank's kernels, then for every
+        rank's.  After it no sweep of a neighbour still stores into this rank's
+        peer buffers over xGMI, so close() may free them.  Reference: nothing
+        (single process)."""
         if self._peers is None:
             return
+        torch.cuda.synchronize(eng.dev)
+        dist.barrier(group=self.group)
+
+    def close(self):
+        """Free / unmap the peer buffers (at exit).  Every fit() ended with
+        quiesce(), so no kernel of any rank writes them any more; the local
+        synchronize covers a process that leaves without finishing a fit()."""
+        if self._peers is None:
+            return
+        try:
+            torch.cuda.synchronize()
+        except Exception:
+            pass
         for p in self._peers:
             if p is not None:
                 p.close()

@@ -37,8 +37,7 @@ from __future__ import annotations
 import collections
 import ctypes
 import math
-import os
-from dataclasses import dataclass
+from dataclasses import dataclass, fields
 from typing import Optional
 
 import torch
@@ -57,6 +56,64 @@ class Shard:
     T_total: int
     rank: int = 0
     world: int = 1
+
+
+@dataclass
+class EngineOptions:
+    """Execution choices of one engine.  Nothing is read from the environment:
+    the defaults are the production path, tests and A/B runs pass these
+    explicitly (``engine_options=`` of the VI classes).
+
+    sweep_kernel  request code of include/ame_amd.h (``_lib.AME_SWEEP_*``):
+                  AUTO picks v3 when the shape fits it, else v2 (with GEMV
+                  workers when they are co-resident)
+    pipeline      queue the next sweep while this one runs (kernels that order
+                  themselves slice by slice on the device)
+    speculate     start the next sweep before this iteration's ELBO is read
+    spec_depth    sweeps kept started ahead of the committed state when
+                  pipelined; None derives it from the global slice count
+                  (:func:`derive_spec_depth`)
+    slice_group   at most this many local slices per launch (0: as many as fit)
+    pairs_kernel  ELBO pair kernel (``_lib.AME_PAIRS_*``; 0 = default)
+    """
+    sweep_kernel: int = 0
+    pipeline: bool = True
+    speculate: bool = True
+    spec_depth: Optional[int] = None
+    slice_group: int = 0
+    pairs_kernel: int = 0
+
+    @classmethod
+    def coerce(cls, opts) -> "EngineOptions":
+        if opts is None:
+            return cls()
+        if isinstance(opts, cls):
+            return opts
+        names = {f.name for f in fields(cls)}
+        bad = set(opts) - names
+        if bad:
+            raise ValueError(f"unknown engine option(s) {sorted(bad)}; known: {sorted(names)}")
+        return cls(**opts)
+
+
+# Queue-depth model (DESIGN.md §5).  In the pipelined steady state with period
+# P (about one slice's chain of n node steps) the host reads iteration k's ELBO
+# once sweep k has finished on the LAST slice of the LAST rank, i.e. after the
+# wavefront's fill over all T_total slices plus one chain plus the ELBO kernels
+# and the all_reduce; by then sweep k + 1 + depth must already be queued:
+#     (1 + depth) P >= fill + C + delta,   fill = F (T_total - 1) steps.
+# F = 2.6 node steps of lag per slice (lane start offset 6.6 us at 2.6 us per
+# step, profiles/r01_s3_sweep3_stamps.txt); delta ~ 128 steps (0.33 ms).
+FILL_STEPS_PER_SLICE = 2.6
+ELBO_READ_STEPS = 128
+MAX_SPEC_DEPTH = 8
+
+
+def derive_spec_depth(n: int, T_total: int) -> int:
+    """Smallest queue depth the model above needs, at least 2 (measured best on
+    one GPU), at most MAX_SPEC_DEPTH."""
+    need = math.ceil((FILL_STEPS_PER_SLICE * (T_total - 1) + ELBO_READ_STEPS) / max(1, n))
+    return max(2, min(MAX_SPEC_DEPTH, need))
 
 
 def _ptr(t: Optional[torch.Tensor]):
@@ -148,7 +205,7 @@ class DeviceEngine:
 
     def __init__(self, model, variant: str, lr: float, X_mean: torch.Tensor,
                  X_cov: torch.Tensor, device=None, shard: Optional[Shard] = None,
-                 halo=None):
+                 halo=None, options: Optional[EngineOptions] = None):
         if not torch.cuda.is_available():
             raise RuntimeError("ame_amd: no GPU visible; the HIP path has no CPU fallback")
         self.L = _lib.lib()
@@ -164,6 +221,7 @@ class DeviceEngine:
             "cuda", torch.cuda.current_device())
         self.shard = shard or Shard(0, self.T, self.T)
         self.halo = halo
+        self.options = opt = EngineOptions.coerce(options)
         self.lr = float(lr)
         self.C = Constants(model)
         sh = self.shard
@@ -189,34 +247,44 @@ class DeviceEngine:
             self.out = torch.zeros(8, dtype=torch.float64, device=dev)
             self.status = torch.zeros(1, dtype=torch.int32, device=dev)
         self.epoch = 0
-        self.max_slices = int(self.L.ame_sweep_max_slices(self.n, self.r))
+        self.max_slices = int(self.L.ame_sweep_max_slices(self.n, self.r, opt.sweep_kernel))
         if self.max_slices < 1:
-            raise RuntimeError(f"ame_amd: no sweep kernel fits n={self.n}, r={self.r}")
-        self.groups = slice_groups(sh.T_local, self.max_slices,
-                                   int(os.environ.get("AME_SLICE_GROUP", "0")))
-        # the groups of a sweep run one after another and share the scratch
+            raise RuntimeError(f"ame_amd: no sweep kernel fits n={self.n}, r={self.r} "
+                               f"(request {opt.sweep_kernel})")
+        self.groups = slice_groups(sh.T_local, self.max_slices, opt.slice_group)
+        # the kernel of each group size is resolved ONCE here and passed with
+        # every launch (ame_sweep rejects a launch whose buffers were sized for
+        # another kind); the groups of a sweep run one after another and share
+        # the scratch
+        self.group_kinds = {}
         sws = 1
         for size in sorted({sz for _, sz in self.groups}):
             gd = _lib.ame_dims(self.n, self.r, size, sh.t_begin, sh.T_total, self.vcode)
-            w = int(self.L.ame_sweep_work_size(ctypes.byref(gd)))
+            k = int(self.L.ame_sweep_kind(ctypes.byref(gd), opt.sweep_kernel))
+            if k < 0:
+                _lib.check(-1, "ame_sweep_kind")
+            w = int(self.L.ame_sweep_work_size(ctypes.byref(gd), k))
             if w < 0:
                 _lib.check(-1, "ame_sweep_work_size")
+            self.group_kinds[size] = k
             sws = max(sws, w)
         self.sweep_work = torch.empty(sws, dtype=torch.float64, device=dev)
-        self.sweep_kind = int(self.L.ame_sweep_kind(ctypes.byref(self.dims)))
+        self.sweep_kind = self.group_kinds[self.groups[0][1]]
         self._out_host = None
         self._out_valid = False
         self.timing = False       # record HIP events around each kernel launch
         self.events = []          # (name, start, end) while timing
-        self.speculation = os.environ.get("AME_SPECULATE", "1") != "0"
+        self.speculation = bool(opt.speculate)
         self._specs = collections.deque()   # (done-event, ring slot) of sweeps started ahead
         # consecutive sweeps alternate between two high-priority streams
         self.sweep_streams = [torch.cuda.Stream(device=self.dev, priority=-1) for _ in range(2)]
         self.done = torch.zeros(max(sh.T_local, 1), dtype=torch.int32, device=self.dev)
-        self.pipelined = (bool(self.L.ame_sweep_orders_slices(self.n, self.r))
+        kinds = set(self.group_kinds.values())
+        self.pipelined = (len(kinds) == 1
+                          and bool(self.L.ame_sweep_orders_slices(self.n, self.r, self.sweep_kind))
                           and len(self.groups) == 1
                           and 2 * sh.T_local <= self.max_slices
-                          and os.environ.get("AME_PIPELINE", "1") != "0")
+                          and bool(opt.pipeline))
         if self.halo is not None:   # every rank must take the same path
             self.pipelined = self.halo.agree(self, self.pipelined)
         # How many sweeps may run ahead of the committed state.  Pipelined sweeps
@@ -224,9 +292,12 @@ class DeviceEngine:
         # its fill over all T slices (all ranks) exceeds one iteration: the host
         # reads iteration k's ELBO only after sweep k has finished everywhere, and
         # sweep k+depth must already be queued by then.
-        self.spec_depth = int(os.environ.get("AME_SPEC_DEPTH", "2" if self.pipelined else "1"))
+        if opt.spec_depth is None:
+            self.spec_depth = derive_spec_depth(self.n, sh.T_total) if self.pipelined else 1
+        else:
+            self.spec_depth = int(opt.spec_depth)
         if self.spec_depth < 1:
-            raise ValueError("AME_SPEC_DEPTH must be >= 1")
+            raise ValueError("spec_depth must be >= 1")
         if not self.pipelined:
             # A sweep that does not order itself slice by slice on the device must
             # not start before the sweep that writes its input slot has finished;
@@ -335,6 +406,7 @@ class DeviceEngine:
             g_next_old = next_old if g == last else at(self.xs[src], off + size, nd, 4)
             dims = _lib.ame_dims(n, self.r, size, sh.t_begin + off, sh.T_total, self.vcode)
             a = _lib.ame_sweep_args(
+                kind=self.group_kinds[size], work_doubles=self.sweep_work.numel(),
                 Yt=at(self.Yt, off, nn2, 4), x_old=at(self.xs[src], off, nd, 4),
                 x_new=at(self.xs[dst], off, nd, 4), next_old=g_next_old,
                 hand=at(self.hand, off, nd, 8), halo_in=g_halo_in, halo_out=g_halo_out,
@@ -395,17 +467,26 @@ class DeviceEngine:
         self._toc(tok)
         self._cov_terms_valid = True
 
-    def launch_elbo(self):
-        if not getattr(self, "_cov_terms_valid", False):
+    def launch_elbo(self, pairs_only=False):
+        """The ELBO / MSE sums of the current state into self.out.  pairs_only
+        (diagnostic timing): the pair kernel alone through ame_elbo_pairs_diag,
+        which writes no sums."""
+        if not pairs_only and not getattr(self, "_cov_terms_valid", False):
             self.refresh_cov_terms()
         prev_final = None
-        if self.halo is not None:
+        if self.halo is not None and not pairs_only:
             prev_final = self.halo.prev_final(self)
         e = _lib.ame_elbo_args(
             Yt=_ptr(self.Yt), x=_ptr(self.x_a), prev_final=prev_final,
             cov_terms=_ptr(self.cov_terms), consts=_ptr(self.consts), phi=_ptr(self.phi),
             rinv=self.C.rinv4(), swap_consistent=1 if self.swap_consistent else 0,
-            work=_ptr(self.work), out=_ptr(self.out))
+            work=_ptr(self.work), out=_ptr(self.out), pairs_kernel=self.options.pairs_kernel)
+        if pairs_only:
+            tok = self._tic("pairs")
+            _lib.check(self.L.ame_elbo_pairs_diag(ctypes.byref(self.dims), ctypes.byref(e),
+                                                  self._sp()), "ame_elbo_pairs_diag")
+            self._toc(tok)
+            return
         tok = self._tic("elbo")
         _lib.check(self.L.ame_elbo(ctypes.byref(self.dims), ctypes.byref(e), self._sp()),
                    "ame_elbo")

@@ -23,7 +23,7 @@ from typing import Optional
 import torch
 
 from .base import BaseTemporalVariationalInference
-from ..engine import DeviceEngine
+from ..engine import DeviceEngine, EngineOptions
 
 
 def default_device():
@@ -38,9 +38,11 @@ def default_device():
 class DeviceTemporalVI(BaseTemporalVariationalInference):
     _variant = "good"
 
-    def __init__(self, model, learning_rate, seed, device=None, distributed=None):
+    def __init__(self, model, learning_rate, seed, device=None, distributed=None,
+                 engine_options=None):
         self._device = device
         self._distributed = distributed
+        self._engine_options = EngineOptions.coerce(engine_options)
         self._engine: Optional[DeviceEngine] = None
         self._host = {"mean": None, "cov": None}
         self._ver = {"mean": None, "cov": None}
@@ -110,7 +112,8 @@ class DeviceTemporalVI(BaseTemporalVariationalInference):
             dev = self._device if self._device is not None else default_device()
             shard, halo = self._make_halo()
             self._engine = DeviceEngine(self.model, self._variant, self.lr, self._host["mean"],
-                                        self._host["cov"], device=dev, shard=shard, halo=halo)
+                                        self._host["cov"], device=dev, shard=shard, halo=halo,
+                                        options=self._engine_options)
             self._ver["mean"] = self._host["mean"]._version
             self._ver["cov"] = self._host["cov"]._version
             self._halo = halo
@@ -147,6 +150,11 @@ class DeviceTemporalVI(BaseTemporalVariationalInference):
         self._spec_next = 0
         if self._engine is not None:
             self._engine.discard_speculation()
+            halo = getattr(self, "_halo", None)
+            if halo is not None:
+                # no rank leaves fit() while a neighbour's dropped sweep may still
+                # store into its peer buffers (they are freed at close / exit)
+                halo.quiesce(self._engine)
 
     def _terms(self):
         return self._ensure_engine().terms(speculate=getattr(self, "_spec_next", 0))

@@ -16,9 +16,10 @@ class TemporalAMENaiveMFVI(DeviceTemporalVI):
     _variant = "naive"
 
     def __init__(self, model, learning_rate: float = 1.0, init_scale: float = 0.1,
-                 seed: int = 42, device=None, distributed=None):
+                 seed: int = 42, device=None, distributed=None, engine_options=None):
         self.init_scale = init_scale
-        super().__init__(model, learning_rate, seed, device=device, distributed=distributed)
+        super().__init__(model, learning_rate, seed, device=device, distributed=distributed,
+                         engine_options=engine_options)
 
     def _initialize_variational_params(self) -> None:
         """naive_mf.py:71-87 (no RNG draw for the covariances)."""

@@ -17,18 +17,22 @@ from ._device_vi import DeviceTemporalVI
 
 class TemporalAMEStructuredMFVI(DeviceTemporalVI):
     """Parameters follow structured_mf.py:58-72.  Extra (build-only) keyword
-    arguments: ``device`` (default: current / LOCAL_RANK GPU) and
+    arguments: ``device`` (default: current / LOCAL_RANK GPU),
     ``distributed`` (None = time-shard automatically when torch.distributed is
-    initialised with world_size > 1)."""
+    initialised with world_size > 1) and ``engine_options``
+    (:class:`ame_amd.engine.EngineOptions` or a dict of its fields: sweep
+    kernel, pipelining, queue depth; the defaults are the production path)."""
 
     def __init__(self, model, factorization: Literal["good", "bad"] = "good",
                  learning_rate: float = 1.0, init_scale: float = 0.1,
-                 cov_init_scale: float = 0.5, seed: int = 42, device=None, distributed=None):
+                 cov_init_scale: float = 0.5, seed: int = 42, device=None, distributed=None,
+                 engine_options=None):
         self.factorization = factorization
         self.init_scale = init_scale
         self.cov_init_scale = cov_init_scale
         self._variant = factorization
-        super().__init__(model, learning_rate, seed, device=device, distributed=distributed)
+        super().__init__(model, learning_rate, seed, device=device, distributed=distributed,
+                         engine_options=engine_options)
 
     # (node, time) blocks per chunk of the covariance init: the arithmetic runs
     # chunk by chunk into the preallocated X_cov, so host memory stays at one

@@ -117,14 +117,30 @@ class TemporalAMEModel:
             self.X[i, 0] = sample(L0, z_d, d)
             for t in range(1, T):
                 self.X[i, t] = torch.matmul(self.Phi, self.X[i, t - 1]) + sample(LQ, z_d, d)
+        # Observation noise (temporal_ame.py:203-214): one 2-vector draw per
+        # upper-triangle dyad, t-major then i then j.  A CPU normal_() call on
+        # fewer than 16 floats takes the scalar Box-Muller path, which caches the
+        # pair's second value, so calls of 14 floats (7 dyads) consume the stream
+        # exactly like 7 calls of 2.  L R^{1/2} eps with the lower-triangular
+        # factor is [L00 e0, L11 e1 + L10 e0] rounded as the reference's 2x2 matvec
+        # rounds it (the second entry as one fused multiply-add onto the rounded
+        # L10 e0 product), checked bit for bit against the reference's Y.
+        iu = torch.triu_indices(n, n, 1)
+        npairs = iu.shape[1]
+        eps = torch.empty(npairs * 2)
+        l00, l10, l11 = (float(LR[0, 0]), float(LR[1, 0]), float(LR[1, 1]))
         for t in range(T):
+            for k in range(0, npairs * 2, 14):
+                eps[k:k + 14].normal_()
+            e = eps.view(npairs, 2).double()
+            p0 = (l00 * e[:, 0]).float()
+            p10 = (l10 * e[:, 0]).float()
+            p1 = (l11 * e[:, 1] + p10.double()).float()
             mu_t = self.compute_mean(self.X[:, t, :2], self.X[:, t, 2:])
-            for i in range(n):
-                for j in range(i + 1, n):
-                    dyad = mu_t[i, j] + sample(LR, z_2, 2)
-                    self.Y[i, j, t] = dyad
-                    self.Y[j, i, t, 0] = dyad[1]
-                    self.Y[j, i, t, 1] = dyad[0]
+            dy = mu_t[iu[0], iu[1]] + torch.stack([p0, p1], dim=1)
+            self.Y[iu[0], iu[1], t] = dy
+            self.Y[iu[1], iu[0], t, 0] = dy[:, 1]
+            self.Y[iu[1], iu[0], t, 1] = dy[:, 0]
         if return_latents:
             return self.Y, self.X
         return self.Y

@@ -45,13 +45,33 @@ def test_host_only_entry_points():
     # every latent dim 1..32 is compiled (the reference takes any r,
     # temporal_ame.py:114-120); the split build routes each r to its part
     assert list(rs) == list(range(1, 33))
-    for r in (9, 10, 17, 31):
-        assert lib.ame_sweep_lds_bytes(64, r) > 0
-    # LDS budget of the sweep's per-slice state: config 3 (n=1024, r=16) fits one CU
-    assert 0 < lib.ame_sweep_lds_bytes(1024, 16) <= 160 * 1024
-    assert lib.ame_sweep_lds_bytes(1024, 999) == 0
+    for r in (9, 10, 17, 31, 32):
+        assert lib.ame_sweep_lds_bytes(64, r, L.AME_SWEEP_V2_LDS) > 0
+    # LDS budget of the v2 sweep's per-slice state: config 3 (n=1024, r=16) fits one CU
+    assert 0 < lib.ame_sweep_lds_bytes(1024, 16, L.AME_SWEEP_V2_LDS) <= 160 * 1024
+    assert lib.ame_sweep_lds_bytes(1024, 999, L.AME_SWEEP_V2_LDS) == 0
+    assert lib.ame_sweep_lds_bytes(1024, 16, 7) == 0              # not a concrete kind
     d = L.ame_dims(1024, 16, 128, 0, 128, L.AME_GOOD)
     assert lib.ame_elbo_work_size(ctypes.byref(d)) > 0
+    # scratch of each concrete kind (host arithmetic, no device query)
+    assert lib.ame_sweep_work_size(ctypes.byref(d), L.AME_SWEEP_V2_LDS) == 0
+    assert lib.ame_sweep_work_size(ctypes.byref(d), L.AME_SWEEP_V2_HBM) == 128 * 1024 * 32 // 2
+    assert lib.ame_sweep_work_size(ctypes.byref(d), L.AME_SWEEP_V2_WORKERS) == 128 * 7 * 8 * 34
+    assert lib.ame_sweep_work_size(ctypes.byref(d), 2) == -1     # a request, not a kind
+
+
+def test_worker_partial_tag_never_zero():
+    """GEMV-worker partial tags (ame_common.h ame_gw_tag): a slot the launch
+    zeroed must never carry a valid tag, including epoch 65536 (whose low 16
+    bits are 0) for node 0."""
+    lib = _lib().lib()
+    for epoch in (1, 2, 32768, 65535, 65536, 65537, 2 ** 31, 2 ** 32 - 1):
+        for m in (0, 1, 7, 4095, 65535):
+            tag = lib.ame_debug_gw_tag(epoch, m)
+            assert tag != 0 and (tag & 0xFFFF) == m
+    # consecutive epochs (one launch each) and ring neighbours m, m + 8 differ
+    assert lib.ame_debug_gw_tag(65536, 0) != lib.ame_debug_gw_tag(65537, 0)
+    assert lib.ame_debug_gw_tag(5, 0) != lib.ame_debug_gw_tag(5, 8)
 
 
 def test_argument_validation_fails_loudly():

@@ -1,0 +1,41 @@
+"""Host-side engine logic (no GPU): explicit options, the queue-depth model,
+slice groups.  DESIGN.md §5."""
+import pytest
+
+from ame_amd.engine import EngineOptions, derive_spec_depth, slice_groups
+
+
+def test_options_are_explicit():
+    o = EngineOptions.coerce(None)
+    assert o == EngineOptions()
+    assert EngineOptions.coerce({"spec_depth": 3}).spec_depth == 3
+    assert EngineOptions.coerce(o) is o
+    with pytest.raises(ValueError, match="unknown engine option"):
+        EngineOptions.coerce({"spec_dpeth": 3})
+
+
+def test_queue_depth_model():
+    """(1 + depth) P >= fill + C + delta with P ~ C = n steps."""
+    # config 3 on one GPU and the weak-scaling series (T = 128 per GPU)
+    assert derive_spec_depth(1024, 128) == 2
+    assert derive_spec_depth(1024, 256) == 2
+    assert derive_spec_depth(1024, 512) == 2
+    assert derive_spec_depth(1024, 1024) == 3      # N = 8: fill 2.6 x 1023 steps > 2 chains
+    # the model's margin at N = 8 and depth 3: (1 + 3) n >= 2.6 (T - 1) + n + 128
+    n, T = 1024, 1024
+    assert (1 + 3) * n >= 2.6 * (T - 1) + n + 128
+    assert (1 + 2) * n < 2.6 * (T - 1) + n + 128   # depth 2 would stall
+    # short chains, many slices: deeper, capped
+    assert derive_spec_depth(256, 512) == 6
+    assert derive_spec_depth(16, 4096) == 8
+    assert derive_spec_depth(4096, 32) == 2
+
+
+def test_slice_groups_cover_in_order():
+    for T, cap, force in [(512, 256, 0), (10, 256, 3), (7, 7, 0), (300, 128, 0), (5, 256, 128)]:
+        g = slice_groups(T, cap, force)
+        assert sum(sz for _, sz in g) == T
+        assert all(b[0] == a[0] + a[1] for a, b in zip(g, g[1:]))
+        assert max(sz for _, sz in g) <= (cap if force <= 0 else min(force, cap))
+    with pytest.raises(RuntimeError):
+        slice_groups(4, 0)

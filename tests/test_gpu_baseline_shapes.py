@@ -32,12 +32,13 @@ pytestmark = pytest.mark.gpu
 PKEYS = ("R", "R_inv", "Sigma", "Psi", "Phi", "Q")
 
 
-def _vi(model, method, lr, dev, distributed=None):
+def _vi(model, method, lr, dev, distributed=None, **opts):
     from ame_amd import TemporalAMENaiveMFVI, TemporalAMEStructuredMFVI
     if method == "naive":
-        return TemporalAMENaiveMFVI(model, learning_rate=lr, device=dev, distributed=distributed)
+        return TemporalAMENaiveMFVI(model, learning_rate=lr, device=dev, distributed=distributed,
+                                    engine_options=opts)
     return TemporalAMEStructuredMFVI(model, factorization=method, learning_rate=lr, device=dev,
-                                     distributed=distributed)
+                                     distributed=distributed, engine_options=opts)
 
 
 def _params(m, dtype=np.float64):
@@ -84,7 +85,7 @@ def test_config3_schedule_prefix_and_elbo(gpu_device):
     # production schedule: one fit() call, sweeps started ahead and pipelined
     m = _config3(gpu_device)
     prod = _vi(m, "good", lr, gpu_device)
-    assert prod.engine.pipelined and prod.engine.spec_depth == 2
+    assert prod.engine.pipelined and prod.engine.spec_depth == 2   # derived: 1 GPU, T = 128
     hp = prod.fit(max_iter=3, tolerance=0.0, verbose=False)
     prod_mean = prod.X_mean.numpy().copy()
     prod_cov_digest = hashlib.sha256(prod.X_cov.numpy().tobytes()).hexdigest()
@@ -92,8 +93,7 @@ def test_config3_schedule_prefix_and_elbo(gpu_device):
     torch.cuda.empty_cache()
     # in-order schedule, one iteration per fit() call, no speculation
     m = _config3(gpu_device)
-    vi = _vi(m, "good", lr, gpu_device)
-    vi.engine.speculation = False
+    vi = _vi(m, "good", lr, gpu_device, speculate=False)
     vi.fit(max_iter=2, tolerance=0.0, verbose=False)
     Xm = vi.X_mean.numpy().astype(np.float64).copy()
     Xc = vi.X_cov.numpy().astype(np.float64).copy()
@@ -188,12 +188,11 @@ def test_config4_rank_shape_two_ranks(gpu_device):
 
 # ---------------- config 4 on one GPU: T=512 > co-resident slices ----------------
 def _c4full_run(distributed, group):
-    os.environ["AME_SLICE_GROUP"] = group
     from ame_amd import TemporalAMEModel
     dev = torch.device("cuda", 0)
     m = TemporalAMEModel(1024, 512, 16, seed=42)
     m.generate_data_fast(device=dev, seed=42)
-    vi = _vi(m, "good", 0.01, dev, distributed=distributed)
+    vi = _vi(m, "good", 0.01, dev, distributed=distributed, slice_group=group)
     groups = len(vi.engine.groups)
     h = vi.fit(max_iter=2, tolerance=0.0, verbose=False)
     mean = vi.X_mean.numpy().copy()
@@ -206,7 +205,7 @@ def _c4full_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        out = _c4full_run(True, "128")   # two groups per rank: both ranks fit on the chip
+        out = _c4full_run(True, 128)   # two groups per rank: both ranks fit on the chip
         if rank == 0:
             q.put(out)
     finally:
@@ -238,10 +237,105 @@ def test_config4_full_T_one_gpu(gpu_device):
             p.join()
     assert codes == [0, 0], f"rank exit codes {codes}"
     mean_d, dig_d, elbo_d, rec_d, groups_d = result
-    mean_s, dig_s, elbo_s, rec_s, groups_s = _c4full_run(False, "0")
-    os.environ.pop("AME_SLICE_GROUP", None)
+    mean_s, dig_s, elbo_s, rec_s, groups_s = _c4full_run(False, 0)
     assert groups_s >= 2 and groups_d == 2
     assert np.array_equal(mean_d, mean_s)
     assert dig_d == dig_s
     assert np.allclose(elbo_d, elbo_s, rtol=1e-6, atol=0)
     assert np.allclose(rec_d, rec_s, rtol=1e-12, atol=0)
+
+
+# ---------------- config 5's per-rank shape (n=4096, T_local=32, r=32) ----------------
+def _replay_prefix(Y32, x0, c0, params64, params32, method, lr, K, T):
+    """The fp64 and fp32 oracle's replay of nodes 0..K-1 of one sweep from the
+    pre-sweep state (node i depends only on that state and on nodes < i,
+    SURVEY.md App. B).  Y stays fp32 (observation_terms promotes the row)."""
+    import ame_oracle as O
+    Xm, Xm32 = x0.astype(np.float64), x0.copy()
+    Xc, Xc32 = c0[:K].astype(np.float64), c0[:K].copy()
+    c64, c32 = O.prior_terms(params64, T, np.float64), O.prior_terms(params32, T, np.float32)
+    for i in range(K):
+        O.update_node(Y32, Xm, Xc, params64, i, method, lr, c64)
+        O.update_node(Y32, Xm32, Xc32, params32, i, method, lr, c32)
+    return Xm[:K], Xc, Xm32[:K].astype(np.float64)
+
+
+def _check_prefix(got_m, got_c, ref_m, ref_c, ref_m32):
+    fp32_err = np.abs(ref_m32 - ref_m).max()
+    err = np.abs(got_m.astype(np.float64) - ref_m).max()
+    assert err <= max(5e-6 * max(1.0, np.abs(ref_m).max()), fp32_err), (err, fp32_err)
+    cerr = np.abs(got_c.astype(np.float64) - ref_c).max()
+    assert cerr <= 1e-6 * max(1.0, np.abs(ref_c).max()), cerr
+    return err, fp32_err
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("method", ["good", "bad", "naive"])
+def test_config5_rank_shape(method, gpu_device):
+    """BASELINE config 5 per rank: n=4096, T_local=32, r=32 (d=66), lr=0.01 --
+    the v2 sweep with seven GEMV worker workgroups per slice on the full chip
+    (32 x 8 = 256 workgroups).
+    * the first K=12 nodes of every slice of the second sweep against the
+      fp64 oracle's replay (past the workers' look-behind: partial m uses node
+      j's NEW mean for j <= m-4, so nodes 4..11 take that path);
+    * every node of that sweep against the single-workgroup v2 sweep (kind 21,
+      its own h_obs order, checked against the oracle at small n and on the
+      config-5 prefix in test_gpu_large.py): agreement to fp32 summation-order
+      round-off (bound 2e-5 * max|mu|; a node-order error is O(lr |mu|));
+    * the device ELBO / MSE of the final state against the CPU ELBO of that
+      same state (tests/elbo_check.py, 5e-6 relative).
+    Reference: naive_mf.py:207-282, structured_mf.py:211-326, :115-209."""
+    from elbo_check import elbo_and_mse
+    from ame_amd import TemporalAMEModel, _lib
+    n, T, r, lr, K = 4096, 32, 32, 0.01, 12
+    m = TemporalAMEModel(n, T, r, seed=42)
+    m.generate_data_fast(device=gpu_device, seed=42)
+    vi = _vi(m, method, lr, gpu_device)
+    assert vi.engine.sweep_kind == _lib.AME_SWEEP_V2_WORKERS and not vi.engine.pipelined
+    vi.fit(max_iter=1, tolerance=0.0, verbose=False)
+    x1, c1 = vi.X_mean.numpy().copy(), vi.X_cov.numpy().copy()
+    h = vi.fit(max_iter=1, tolerance=0.0, verbose=False)
+    got_m, got_c = vi.X_mean.numpy().copy(), vi.X_cov.numpy()
+    # independent kernel, same start state, one sweep
+    ref = _vi(m, method, lr, gpu_device, sweep_kernel=_lib.AME_SWEEP_V2_SINGLE)
+    assert ref.engine.sweep_kind == _lib.AME_SWEEP_V2_HBM
+    ref.X_mean = torch.from_numpy(x1.copy())
+    ref.X_cov = torch.from_numpy(c1.copy())
+    ref.fit(max_iter=1, tolerance=0.0, verbose=False)
+    d_all = np.abs(ref.X_mean.numpy() - got_m).max()
+    assert d_all <= 2e-5 * max(1.0, np.abs(got_m).max()), d_all
+    del ref
+    torch.cuda.empty_cache()
+    Y32 = m.Y.cpu().numpy()
+    rm, rc, rm32 = _replay_prefix(Y32, x1, c1, _params(m), _params(m, np.float32), method, lr, K, T)
+    _check_prefix(got_m[:K], got_c[:K], rm, rc, rm32)
+    e = elbo_and_mse(Y32, got_m, got_c, _params(m), method)
+    assert abs(float(h["elbo"][-1]) - e["elbo"]) <= 5e-6 * abs(e["elbo"]), (float(h["elbo"][-1]), e)
+    assert abs(h["reconstruction_error"][-1] - e["recon"]) <= 5e-6 * e["recon"]
+
+
+# ---------------- config 4 at full T on one GPU: oracle prefix ----------------
+@pytest.mark.timeout(600)
+def test_config4_full_T_oracle_prefix(gpu_device):
+    """BASELINE config 4 (n=1024, T=512, r=16, lr=0.01) in one process: the
+    512 slices run as consecutive slice groups.  The third sweep's first K=8
+    nodes of ALL 512 slices against the fp64 oracle's replay, and the device
+    ELBO / MSE against the CPU ELBO of the device state.
+    Reference: structured_mf.py:211-326, :115-209, temporal_ame.py:255-291."""
+    from elbo_check import elbo_and_mse
+    from ame_amd import TemporalAMEModel
+    n, T, r, lr, K = 1024, 512, 16, 0.01, 8
+    m = TemporalAMEModel(n, T, r, seed=42)
+    m.generate_data_fast(device=gpu_device, seed=42)
+    vi = _vi(m, "good", lr, gpu_device)
+    assert len(vi.engine.groups) >= 2
+    vi.fit(max_iter=2, tolerance=0.0, verbose=False)
+    x2, c2 = vi.X_mean.numpy().copy(), vi.X_cov.numpy().copy()
+    h = vi.fit(max_iter=1, tolerance=0.0, verbose=False)
+    got_m, got_c = vi.X_mean.numpy(), vi.X_cov.numpy()
+    Y32 = m.Y.cpu().numpy()
+    rm, rc, rm32 = _replay_prefix(Y32, x2, c2, _params(m), _params(m, np.float32), "good", lr, K, T)
+    _check_prefix(got_m[:K], got_c[:K], rm, rc, rm32)
+    e = elbo_and_mse(Y32, got_m, got_c, _params(m), "good")
+    assert abs(float(h["elbo"][-1]) - e["elbo"]) <= 5e-6 * abs(e["elbo"]), (float(h["elbo"][-1]), e)
+    assert abs(h["reconstruction_error"][-1] - e["recon"]) <= 5e-6 * e["recon"]

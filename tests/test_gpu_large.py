@@ -2,8 +2,8 @@
 
 * r = 32 (d = 66 > 64: two state rows per solver lane), BASELINE config 5's
   latent dim, against the fp64 oracle on small problems, all three variants;
-* the slice's (U,V) block read from HBM instead of LDS (forced with
-  AME_SWEEP_M_GLOBAL=1 at small n; automatic at n = 4096);
+* the slice's (U,V) block read from HBM instead of LDS (kind AME_SWEEP_V2_HBM
+  requested at small n; automatic at n = 3400);
 * config 5's node count and latent dim (n = 4096, r = 32) on a few slices:
   the first nodes of the Gauss-Seidel sweep against the oracle replaying the
   same sweep prefix (node i depends only on the initial state and on nodes < i,
@@ -21,23 +21,24 @@ pytestmark = pytest.mark.gpu
 PKEYS = ("R", "R_inv", "Sigma", "Psi", "Phi", "Q")
 
 
-def _vi(model, method, lr, dev):
+def _vi(model, method, lr, dev, **opts):
     from ame_amd import TemporalAMENaiveMFVI, TemporalAMEStructuredMFVI
     if method == "naive":
-        return TemporalAMENaiveMFVI(model, learning_rate=lr, device=dev)
-    return TemporalAMEStructuredMFVI(model, factorization=method, learning_rate=lr, device=dev)
+        return TemporalAMENaiveMFVI(model, learning_rate=lr, device=dev, engine_options=opts)
+    return TemporalAMEStructuredMFVI(model, factorization=method, learning_rate=lr, device=dev,
+                                     engine_options=opts)
 
 
 def _params(m, dtype=np.float64):
     return {k: getattr(m, k).numpy().astype(dtype) for k in PKEYS}
 
 
-def _check_vs_oracle(n, T, r, method, lr, dev, iters=2):
+def _check_vs_oracle(n, T, r, method, lr, dev, iters=2, **opts):
     import ame_oracle as O
     from ame_amd import TemporalAMEModel
     m = TemporalAMEModel(n, T, r, seed=7)
     m.generate_data_fast(seed=11)
-    vi = _vi(m, method, lr, dev)
+    vi = _vi(m, method, lr, dev, **opts)
     Xm = vi.X_mean.numpy().astype(np.float64).copy()
     Xc = vi.X_cov.numpy().astype(np.float64).copy()
     Xm32, Xc32 = vi.X_mean.numpy().copy(), vi.X_cov.numpy().copy()
@@ -69,27 +70,29 @@ def test_r32_vs_oracle(n, T, r, method, lr, gpu_device):
 @pytest.mark.parametrize("n,T,r,method,lr", [
     (50, 4, 4, "good", 0.5), (37, 3, 5, "bad", 1.0), (45, 3, 16, "naive", 0.7),
     (30, 3, 32, "good", 0.5), (700, 2, 16, "good", 0.5)])
-def test_global_slice_vs_oracle(n, T, r, method, lr, gpu_device, monkeypatch):
-    """(U,V) block in HBM (AME_SWEEP_M_GLOBAL=1) on the v2 sweep (AME_SWEEP_V2=1)."""
-    monkeypatch.setenv("AME_SWEEP_V2", "1")
-    monkeypatch.setenv("AME_SWEEP_M_GLOBAL", "1")
-    _check_vs_oracle(n, T, r, method, lr, gpu_device)
+def test_global_slice_vs_oracle(n, T, r, method, lr, gpu_device):
+    """(U,V) block in HBM on the single-workgroup v2 sweep (kind 21 requested)."""
+    from ame_amd import _lib
+    vi = _check_vs_oracle(n, T, r, method, lr, gpu_device, sweep_kernel=_lib.AME_SWEEP_V2_HBM)
+    assert vi.engine.sweep_kind == _lib.AME_SWEEP_V2_HBM
 
 
 @pytest.mark.parametrize("n,T,r,method,lr", [(64, 5, 8, "good", 0.5), (33, 4, 3, "bad", 1.0)])
-def test_v2_lds_slice_vs_oracle(n, T, r, method, lr, gpu_device, monkeypatch):
-    """The v2 sweep with the slice in LDS (the path r = 32 takes at small n)."""
-    monkeypatch.setenv("AME_SWEEP_V2", "1")
-    _check_vs_oracle(n, T, r, method, lr, gpu_device)
+def test_v2_lds_slice_vs_oracle(n, T, r, method, lr, gpu_device):
+    """The single-workgroup v2 sweep with the slice in LDS (kind 20)."""
+    from ame_amd import _lib
+    vi = _check_vs_oracle(n, T, r, method, lr, gpu_device, sweep_kernel=_lib.AME_SWEEP_V2_LDS)
+    assert vi.engine.sweep_kind == _lib.AME_SWEEP_V2_LDS
 
 
 def test_auto_global_slice_past_v3(gpu_device):
     """n = 3400, r = 16: past the v3 sweep's register/LDS budget and past the v2
     LDS slice, so the v2 sweep keeps the slice in HBM on its own."""
     from ame_amd import _lib
-    L = _lib.lib()
-    assert L.ame_sweep_orders_slices(3400, 16) == 0          # not the v3 sweep
-    _check_vs_oracle(3400, 1, 16, "good", 0.5, gpu_device, iters=1)
+    vi = _check_vs_oracle(3400, 1, 16, "good", 0.5, gpu_device, iters=1,
+                          sweep_kernel=_lib.AME_SWEEP_V2_SINGLE)
+    assert vi.engine.sweep_kind == _lib.AME_SWEEP_V2_HBM   # past v3 and the LDS slice
+    assert _lib.lib().ame_sweep_orders_slices(3400, 16, vi.engine.sweep_kind) == 0
 
 
 @pytest.mark.parametrize("method", ["good", "bad", "naive"])

@@ -3,7 +3,7 @@ against the register-streaming v1 kernel and the fp64 oracle.
 
 Reference: structured_mf.py:124-150 (expected log-likelihood),
 temporal_ame.py:255-291 (reconstruction error).  v2 runs whenever n is even;
-AME_PAIRS_V1=1 selects v1.  Both form the same fp32 products and per-tile fp32
+engine option pairs_kernel=AME_PAIRS_V1 selects v1.  Both form the same fp32 products and per-tile fp32
 partial sums, so they agree to a few fp32 ulps of the total (bound 1e-6
 relative, stated here); against the fp64 oracle the ELBO log-likelihood and
 the reconstruction error are held to 5e-6 relative, as in test_gpu_parity.py.
@@ -14,9 +14,11 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _sums(vi, monkeypatch, v1):
-    monkeypatch.setenv("AME_PAIRS_V1", "1" if v1 else "0")
+def _sums(vi, v1):
+    from ame_amd import _lib
     eng = vi.engine
+    eng.options.pairs_kernel = _lib.AME_PAIRS_V1 if v1 else _lib.AME_PAIRS_V2
+    eng.invalidate()
     eng.launch_elbo()
     out = eng.out.cpu().numpy().astype(np.float64).copy()
     eng._check_status()
@@ -27,7 +29,7 @@ def _sums(vi, monkeypatch, v1):
     (64, 3, 16, True), (130, 2, 16, True), (200, 3, 8, False), (256, 4, 32, True),
     (1024, 8, 16, True), (1024, 2, 16, False), (2, 3, 1, True), (98, 2, 5, True),
     (192, 5, 3, False), (4096, 1, 32, True)])
-def test_pairs_v2_matches_v1_and_oracle(n, T, r, swap, gpu_device, monkeypatch):
+def test_pairs_v2_matches_v1_and_oracle(n, T, r, swap, gpu_device):
     import ame_oracle as O
     from ame_amd import TemporalAMEModel, TemporalAMEStructuredMFVI
     m = TemporalAMEModel(n, T, r, seed=5)
@@ -38,8 +40,8 @@ def test_pairs_v2_matches_v1_and_oracle(n, T, r, swap, gpu_device, monkeypatch):
     vi = TemporalAMEStructuredMFVI(m, factorization="good", learning_rate=0.3, device=gpu_device)
     assert vi.engine.swap_consistent == swap
     vi.fit(max_iter=1, tolerance=0.0, verbose=False)   # a non-initial state
-    a = _sums(vi, monkeypatch, v1=True)
-    b = _sums(vi, monkeypatch, v1=False)
+    a = _sums(vi, v1=True)
+    b = _sums(vi, v1=False)
     # out[0] = sum of the quadratic form over i<j, out[7] = squared-error sum
     for k in (0, 7):
         assert abs(b[k] - a[k]) <= 1e-6 * abs(a[k]), (k, a[k], b[k])

@@ -32,11 +32,12 @@ def _make(tag):
     return m
 
 
-def _vi(model, method, lr, dev):
+def _vi(model, method, lr, dev, **opts):
     from ame_amd import TemporalAMENaiveMFVI, TemporalAMEStructuredMFVI
     if method == "naive":
-        return TemporalAMENaiveMFVI(model, learning_rate=lr, device=dev)
-    return TemporalAMEStructuredMFVI(model, factorization=method, learning_rate=lr, device=dev)
+        return TemporalAMENaiveMFVI(model, learning_rate=lr, device=dev, engine_options=opts)
+    return TemporalAMEStructuredMFVI(model, factorization=method, learning_rate=lr, device=dev,
+                                     engine_options=opts)
 
 
 def _fixtures():
@@ -198,15 +199,15 @@ def test_deterministic(gpu_device):
     assert outs[0][2] == outs[1][2] and outs[0][3] == outs[1][3]
 
 
-def _twins(n, T, r, method, lr, dev):
-    """Two identical runs: the engine's speculative schedule and the in-order one."""
+def _twins(n, T, r, method, lr, dev, **opts):
+    """Two identical runs: the engine's speculative schedule (with `opts`) and
+    the in-order one."""
     from ame_amd import TemporalAMEModel
     out = []
     for spec in (True, False):
         m = TemporalAMEModel(n, T, r, seed=3)
         m.generate_data_fast(seed=4)
-        vi = _vi(m, method, lr, dev)
-        vi.engine.speculation = spec
+        vi = _vi(m, method, lr, dev, **(opts if spec else {"speculate": False}))
         out.append(vi)
     return out
 
@@ -251,15 +252,14 @@ def test_pipelined_sweeps_many_slices(gpu_device):
     assert [float(e) for e in ha["elbo"]] == [float(e) for e in hb["elbo"]]
 
 
-@pytest.mark.parametrize("depth", ["1", "3"])
-def test_speculation_depth_is_exact(depth, gpu_device, monkeypatch):
+@pytest.mark.parametrize("depth", [1, 3, 5])
+def test_speculation_depth_is_exact(depth, gpu_device):
     """Sweeps queued `depth` deep (state ring of depth + 1 slots, each slice
     waiting on the device for the previous sweep): bit-identical to the
     in-order schedule, also when fit() stops at convergence with sweeps still
     queued, and when a later fit() continues."""
-    monkeypatch.setenv("AME_SPEC_DEPTH", depth)
-    a, b = _twins(90, 40, 4, "good", 0.5, gpu_device)
-    assert a.engine.spec_depth == int(depth) and len(a.engine.xs) == int(depth) + 1
+    a, b = _twins(90, 40, 4, "good", 0.5, gpu_device, spec_depth=depth)
+    assert a.engine.spec_depth == depth and len(a.engine.xs) == depth + 1
     ha = a.fit(max_iter=7, tolerance=0.0, verbose=False)
     hb = b.fit(max_iter=7, tolerance=0.0, verbose=False)
     assert [float(e) for e in ha["elbo"]] == [float(e) for e in hb["elbo"]]
@@ -271,12 +271,10 @@ def test_speculation_depth_is_exact(depth, gpu_device, monkeypatch):
     assert [float(e) for e in a.history["elbo"]] == [float(e) for e in b.history["elbo"]]
 
 
-def test_unpipelined_queue_is_one_deep(gpu_device, monkeypatch):
-    """Sweeps that do not order themselves on the device (AME_PIPELINE=0) are
-    queued one deep whatever AME_SPEC_DEPTH asks, and stay exact."""
-    monkeypatch.setenv("AME_PIPELINE", "0")
-    monkeypatch.setenv("AME_SPEC_DEPTH", "2")
-    a, b = _twins(90, 40, 4, "good", 0.5, gpu_device)
+def test_unpipelined_queue_is_one_deep(gpu_device):
+    """Sweeps that do not order themselves on the device (pipeline=False) are
+    queued one deep whatever spec_depth asks, and stay exact."""
+    a, b = _twins(90, 40, 4, "good", 0.5, gpu_device, pipeline=False, spec_depth=2)
     assert not a.engine.pipelined and a.engine.spec_depth == 1
     ha = a.fit(max_iter=5, tolerance=0.0, verbose=False)
     hb = b.fit(max_iter=5, tolerance=0.0, verbose=False)
@@ -304,19 +302,18 @@ def test_state_attributes_stay_live(gpu_device):
     assert vi.engine.x_a.shape[1] == 40
 
 
-@pytest.mark.parametrize("group", ["3", "4"])
-def test_slice_groups_are_exact(group, gpu_device, monkeypatch):
-    """Local slices launched as consecutive groups (AME_SLICE_GROUP forces the
+@pytest.mark.parametrize("group", [3, 4])
+def test_slice_groups_are_exact(group, gpu_device):
+    """Local slices launched as consecutive groups (slice_group forces the
     size; by default only when T_local exceeds the co-resident workgroups):
     bit-identical to one launch over all slices."""
     from ame_amd import TemporalAMEModel
     outs = []
-    for g in ("0", group):
-        monkeypatch.setenv("AME_SLICE_GROUP", g)
+    for g in (0, group):
         m = TemporalAMEModel(48, 10, 3, seed=12)
         m.generate_data_fast(seed=12)
-        vi = _vi(m, "good", 0.5, gpu_device)
-        assert len(vi.engine.groups) == (1 if g == "0" else -(-10 // int(g)))
+        vi = _vi(m, "good", 0.5, gpu_device, slice_group=g)
+        assert len(vi.engine.groups) == (1 if g == 0 else -(-10 // g))
         h = vi.fit(max_iter=3, tolerance=0.0, verbose=False)
         outs.append((vi.X_mean.numpy().copy(), vi.X_cov.numpy().copy(), [float(e) for e in h["elbo"]]))
     assert np.array_equal(outs[0][0], outs[1][0])

@@ -18,19 +18,24 @@ from test_gpu_large import _check_vs_oracle, _vi
 pytestmark = pytest.mark.gpu
 
 
-def _kind(n, T, r, variant=0):
+def _kind(n, T, r, request=0, variant=0):
     from ame_amd import _lib
     L = _lib.lib()
     d = _lib.ame_dims(n, r, T, 0, T, variant)
-    return int(L.ame_sweep_kind(ctypes.byref(d)))
+    return int(L.ame_sweep_kind(ctypes.byref(d), request))
 
 
-def test_kind_selection(gpu_device, monkeypatch):
+def test_kind_selection(gpu_device):
+    from ame_amd import _lib
     assert _kind(4096, 32, 32) == 22           # config 5 per-rank shape
     assert _kind(1024, 128, 16) == 3           # config 3: v3
     assert _kind(4096, 40, 32) == 21           # 40 x 8 workgroups do not fit: HBM slice
-    monkeypatch.setenv("AME_SWEEP_NOWORKERS", "1")
-    assert _kind(4096, 32, 32) == 21
+    assert _kind(4096, 32, 32, _lib.AME_SWEEP_V2_SINGLE) == 21
+    assert _kind(1024, 128, 16, _lib.AME_SWEEP_V2_AUTO) == 21    # 128 x 8 > co-resident
+    assert _kind(64, 3, 8, _lib.AME_SWEEP_V2_AUTO) == 22
+    assert _kind(4096, 40, 32, _lib.AME_SWEEP_V2_WORKERS) == -1  # refused, not re-routed
+    assert _kind(4096, 32, 32, _lib.AME_SWEEP_V3) == -1          # d = 66 > 64
+    assert _kind(4096, 32, 32, 99) == -1
 
 
 @pytest.mark.parametrize("n,T,r,method,lr", [
@@ -44,31 +49,32 @@ def test_workers_vs_oracle(n, T, r, method, lr, gpu_device):
 
 
 @pytest.mark.parametrize("n,T,r,method,lr", [(64, 3, 8, "good", 0.5), (45, 3, 5, "bad", 1.0)])
-def test_workers_small_r_vs_oracle(n, T, r, method, lr, gpu_device, monkeypatch):
-    """r < 32: lanes >= 2r of a worker wave idle; v2 forced (AME_SWEEP_V2=1)."""
-    monkeypatch.setenv("AME_SWEEP_V2", "1")
-    assert _kind(n, T, r) == 22
-    _check_vs_oracle(n, T, r, method, lr, gpu_device)
+def test_workers_small_r_vs_oracle(n, T, r, method, lr, gpu_device):
+    """r < 32: lanes >= 2r of a worker wave idle; v2 with workers requested."""
+    from ame_amd import _lib
+    assert _kind(n, T, r, _lib.AME_SWEEP_V2_AUTO) == 22
+    vi = _check_vs_oracle(n, T, r, method, lr, gpu_device, sweep_kernel=_lib.AME_SWEEP_V2_WORKERS)
+    assert vi.engine.sweep_kind == 22
 
 
 @pytest.mark.parametrize("n,T,r,method,lr", [(24, 3, 32, "good", 0.5), (30, 3, 32, "naive", 0.5)])
-def test_no_workers_vs_oracle(n, T, r, method, lr, gpu_device, monkeypatch):
-    """AME_SWEEP_NOWORKERS=1 keeps the single-workgroup v2 (kind 20)."""
-    monkeypatch.setenv("AME_SWEEP_NOWORKERS", "1")
-    assert _kind(n, T, r) == 20
-    _check_vs_oracle(n, T, r, method, lr, gpu_device)
+def test_no_workers_vs_oracle(n, T, r, method, lr, gpu_device):
+    """The single-workgroup v2 (kind 20) on a shape that would take workers."""
+    from ame_amd import _lib
+    assert _kind(n, T, r, _lib.AME_SWEEP_V2_SINGLE) == 20
+    vi = _check_vs_oracle(n, T, r, method, lr, gpu_device, sweep_kernel=_lib.AME_SWEEP_V2_SINGLE)
+    assert vi.engine.sweep_kind == 20
 
 
-def test_workers_slice_groups(gpu_device, monkeypatch):
-    """Slices in consecutive groups (AME_SLICE_GROUP=2), each launch with its own
+def test_workers_slice_groups(gpu_device):
+    """Slices in consecutive groups (slice_group=2), each launch with its own
     workers: bit-equal to one launch over all slices."""
     from ame_amd import TemporalAMEModel
     outs = []
-    for g in ("0", "2"):
-        monkeypatch.setenv("AME_SLICE_GROUP", g)
+    for g in (0, 2):
         m = TemporalAMEModel(60, 5, 32, seed=3)
         m.generate_data_fast(seed=4)
-        vi = _vi(m, "good", 0.5, gpu_device)
+        vi = _vi(m, "good", 0.5, gpu_device, slice_group=g)
         assert vi.engine.sweep_kind == 22
         vi.fit(max_iter=2, tolerance=0.0, verbose=False)
         outs.append((vi.X_mean.numpy().copy(), vi.X_cov.numpy().copy()))

@@ -16,8 +16,14 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "python-temporal-ame-svi_amd")
 BDIR = os.path.join(PKG, "ame_amd", "_build")
-SRCS = ("ame_sweep.hip", "ame_sweep3.hip", "ame_sweep4.hip", "ame_cov.hip", "ame_elbo.hip", "ame_capi.hip",
-        "ame_selftest.hip", "ame_align.hip")
+
+def _unsplit_sources():
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "python-temporal-ame-svi_amd"))
+    from ame_amd.build import UNSPLIT_SOURCES
+    return UNSPLIT_SOURCES
+
+SRCS = _unsplit_sources()
 
 
 def build(tag, defs):

@@ -17,8 +17,14 @@ PKG = os.path.join(ROOT, "python-temporal-ame-svi_amd")
 BDIR = os.path.join(PKG, "ame_amd", "_build")
 TAG = ([a.split("=", 1)[1] for a in sys.argv if a.startswith("--tag=")] or [""])[0]
 SO = os.path.join(BDIR, f"libame_amd_stamps3{TAG}.so")
-SRCS = ("ame_sweep.hip", "ame_sweep3.hip", "ame_sweep4.hip", "ame_cov.hip", "ame_elbo.hip", "ame_capi.hip",
-        "ame_selftest.hip", "ame_align.hip")
+
+def _unsplit_sources():
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "python-temporal-ame-svi_amd"))
+    from ame_amd.build import UNSPLIT_SOURCES
+    return UNSPLIT_SOURCES
+
+SRCS = _unsplit_sources()
 NAMES = {
     0: ["start", "J+kj", "reduce", "ddone", "2x2+assembly", "publish", "kcnt", "brow", "gcnt", "prep(v,yv)"],
     1: ["start", "pring", "poll", "hf1", "HB", "GEMV", "spin", "-", "-", "end"],

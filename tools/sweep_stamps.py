@@ -19,6 +19,13 @@ PHASES = ["phase 1: K-matvecs + z staging", "phase 2: wave0 Woodbury | waves1-3 
           "phase 3: K rank-4 update + cov write + AR", "loop (+ cov prefetch issue)"]
 
 
+
+def _unsplit_sources():
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "python-temporal-ame-svi_amd"))
+    from ame_amd.build import UNSPLIT_SOURCES
+    return UNSPLIT_SOURCES
+
 def _opt(name, default=None):
     for a in sys.argv:
         if a.startswith(name + "="):
@@ -34,8 +41,7 @@ def build(r=16):
     tag = _opt("--tag", "")
     so = SO.replace(".so", f"{tag}.so")
     objs = []
-    for src in ("ame_sweep.hip", "ame_sweep3.hip", "ame_sweep4.hip", "ame_cov.hip", "ame_elbo.hip", "ame_capi.hip",
-                "ame_selftest.hip", "ame_align.hip"):
+    for src in _unsplit_sources():
         o = os.path.join(BDIR, src.replace(".hip", f"_stamps{tag}.o"))
         subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17",
                                "-DAME_STAMPS", f"-DAME_ONLY_R={r}", *defs, "-Wno-pass-failed",
