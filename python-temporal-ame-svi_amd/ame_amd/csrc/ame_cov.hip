@@ -5,144 +5,194 @@
 // tr(Q^-1 S_it) (:193).  The covariances are written by the sweep; this kernel
 // reads each stored fp32 covariance once (4 d^2 bytes).
 //
-// Work split (x = [a, b, U(r), V(r)], d = 2 + 2r):
-//  * the (a,b) 2x2 block is eliminated first with its closed-form inverse,
-//    leaving the 2r x 2r Schur complement S = A_xx - A_xa A_aa^-1 A_ax;
-//  * S is factorised LDL^T with column c of S in lane c, so 64 / 2r
-//    covariances share a wave (2 at r = 16) and no lane idles; the pivot row
-//    goes through LDS (one store per lane, broadcast reads back).
+// Work split (x = [a, b, U(r), V(r)], d = 2 + 2r, B = 2r):
+//  * lane l of a covariance's lane group holds column 2 + l of A (rows 0..d-1,
+//    one coalesced row-slice per row); 64 / LPM covariances per wave, LPM the
+//    power of two >= B;
+//  * traces need no elimination: tr A from the diagonal, tr(M A) (M = Q^-1 for
+//    t >= 1, Sigma0^-1 at t = 0) as sum_k M[k][2+l] A[k][2+l] per lane (columns
+//    0, 1 from rows 0, 1 of the lanes' columns: A is symmetric);
+//  * the (a,b) block is eliminated in closed form (the lanes swap their rows
+//    0, 1 through LDS), leaving the B x B Schur complement S, factorised LDL^T
+//    with column l of S in lane l; the pivot row goes through LDS (one store per
+//    lane, broadcast 16-byte reads back).  log|A| = log|A_aa| + sum log pivots,
+//    one product with periodic exponent extraction, one log per covariance;
+//    torch.logdet semantics: -inf for a zero pivot, nan for a negative
+//    determinant.  fp64 throughout;
+//  * persistent waves: each wave walks covariance groups with a grid stride and
+//    loads the next group's columns while it factorises the current one, and
+//    the register footprint allows 2 (r = 32) to 4 (r <= 16) waves per SIMD, so
+//    the per-pivot dependent chain (LDS round trip, reciprocal) of one wave
+//    overlaps other waves' work.  (Round 2's kernel held one group per wave
+//    with no prefetch and spilled at r = 32: 0.61 ms at config 3, 9.9 ms at
+//    config 5's rank shape.)
 // The input is taken as symmetric: the sweep writes symmetric covariances and
 // the reference's initialisation symmetrises (structured_mf.py:94-96).
-// log|A| = log|A_aa| + sum log pivots, accumulated as one product with
-// periodic exponent extraction (one log per covariance); torch.logdet
-// semantics: -inf for a zero pivot, nan for a negative determinant.
 #include "ame_common.h"
 
-template <int B>
-struct CovLanes {   // lanes per covariance: next power of two >= 2r
-    static constexpr int v = B <= 2 ? 2 : B <= 4 ? 4 : B <= 8 ? 8 : B <= 16 ? 16 : B <= 32 ? 32 : 64;
+template <int R>
+struct CovCfg {
+    static constexpr int B = 2 * R, D = B + 2, DD = D * D;
+    static constexpr int LPM = B <= 2 ? 2 : B <= 4 ? 4 : B <= 8 ? 8 : B <= 16 ? 16 : B <= 32 ? 32 : 64;
+    static constexpr int MPW = 64 / LPM;   // covariances per wave-task
+    static constexpr int WPB = 4;          // waves per block
+    // waves per SIMD the registers allow, and whether the next group's column is
+    // loaded during the elimination (B > 32: the column stays in registers only
+    // until the complement is formed; 2 waves per SIMD hide the load instead)
+    static constexpr int WAVES = B > 32 ? 2 : 3;
+    static constexpr bool PREFETCH = B <= 32;
 };
 
-// Waves per SIMD the register budget must allow (the unrolled elimination
-// otherwise takes 364 VGPRs: one wave per SIMD, latency-bound).
-#ifndef AME_COV_WAVES
-#define AME_COV_WAVES 1
-#endif
 template <int R>
-__global__ void __launch_bounds__(AME_NT, AME_COV_WAVES)
+__global__ void __launch_bounds__(256, CovCfg<R>::WAVES)
 ame_cov_kernel(ame_dims dm, ame_cov_args a) {
-    constexpr int D = 2 + 2 * R, B = 2 * R, DD = D * D;
-    constexpr int LPM = CovLanes<B>::v, MPW = 64 / LPM, WPB = AME_NT / 64;
-    __shared__ double qs[2 * DD];                                   // S0inv, Qinv
-    __shared__ __attribute__((aligned(16))) double rows[WPB][64];   // pivot rows
+    using C = CovCfg<R>;
+    constexpr int B = C::B, D = C::D, DD = C::DD, LPM = C::LPM, MPW = C::MPW, WPB = C::WPB;
+    __shared__ __attribute__((aligned(16))) double qs[2 * DD];        // S0inv, Qinv
+    __shared__ __attribute__((aligned(16))) double xb[WPB][3 * 64];   // per wave: pivot row | u0 u1
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    for (int e = tid; e < 2 * DD; e += AME_NT) qs[e] = a.consts[e];
+    for (int e = tid; e < 2 * DD; e += 256) qs[e] = a.consts[e];
     __syncthreads();
     const long long total = (long long)dm.T_local * dm.n;
-    const long long first = ((long long)blockIdx.x * WPB + w) * MPW;
-    if (first >= total) return;   // whole wave; no barrier follows
+    const long long ntask = (total + MPW - 1) / MPW;
+    const long long stride = (long long)gridDim.x * WPB;
     const int sub = lane / LPM, l = lane - sub * LPM;
-    const bool mv = first + sub < total;
-    const long long mc = mv ? first + sub : total - 1;
-    const int tl = (int)(mc / dm.n);
-    const int tg = dm.t_begin + tl;
     const bool lv = l < B;
-    const int c = 2 + (lv ? l : 0);
-    const float* A = a.cov + mc * DD;
-    const double* S0 = qs;
-    const double* Qi = qs + DD;
+    const int lc = lv ? l : B - 1;            // idle lanes shadow the last column
+    double* rb = xb[w] + sub * LPM;            // pivot row of this covariance
+    double* ub = xb[w] + 64 + 2 * sub * LPM;   // (u0, u1) pairs of its lanes
 
-    // the (a,b) block and this lane's column c in rows 0, 1
-    const double a00 = A[0], a01 = A[1], a10 = A[D], a11 = A[D + 1];
-    const double u0 = A[c], u1 = A[D + c];
-    const double det2 = a00 * a11 - a01 * a10;
-    const double id2 = 1.0 / det2;
-    const double w0 = (a11 * u0 - a01 * u1) * id2;   // A_aa^-1 (A_0c, A_1c)
-    const double w1 = (a00 * u1 - a10 * u0) * id2;
-    // traces: column c (rows 0, 1 here, rows >= 2 in the loop) and columns 0, 1
-    // (every lane computes them, lane l == 0 keeps them)
-    double tq = Qi[c] * u0 + Qi[D + c] * u1;
-    double tq0 = Qi[0] * a00 + Qi[1] * a10 + Qi[D] * a01 + Qi[D + 1] * a11;
-    double tr = 0.0;
-    double col[B];
+    // loads of one covariance group: column 2 + lc (rows 0..D-1) and the (a,b) block
+    float v[D], aa[4];
+    auto load = [&](long long task) {
+        const long long mc0 = task * MPW + sub;
+        const long long mc = mc0 < total ? mc0 : total - 1;
+        const float* A = a.cov + mc * DD;
 #pragma unroll
-    for (int k = 0; k < B; ++k) {
-        const float* rk = A + (2 + k) * D;
-        const double x = rk[c], c0 = rk[0], c1 = rk[1];
-        tq = fma(Qi[(2 + k) * D + c], x, tq);
-        tr = (k == l) ? x : tr;
-        tq0 = fma(Qi[2 + k], c0, fma(Qi[D + 2 + k], c1, tq0));
-        col[k] = x - (c0 * w0 + c1 * w1);
-        if ((k & 7) == 7) asm volatile("" ::: "memory");
-    }
-    double ts = 0.0;
-    if (__any(tg == 0)) {   // tr(S0inv A): first time slice only (wave-uniform branch)
-        ts = S0[c] * u0 + S0[D + c] * u1;
-        double ts0 = S0[0] * a00 + S0[1] * a10 + S0[D] * a01 + S0[D + 1] * a11;
+        for (int k = 0; k < D; ++k) v[k] = A[k * D + 2 + lc];
+        aa[0] = A[0];
+        aa[1] = A[1];
+        aa[2] = A[D];
+        aa[3] = A[D + 1];
+    };
+    long long task = (long long)blockIdx.x * WPB + w;
+    if (task >= ntask) return;   // whole wave; no barrier follows
+    if constexpr (C::PREFETCH) load(task);
+    for (; task < ntask; task += stride) {
+        if constexpr (!C::PREFETCH) load(task);
+        const long long mc0 = task * MPW + sub;
+        const bool mv = mc0 < total;
+        const long long mc = mv ? mc0 : total - 1;
+        const int tg = dm.t_begin + (int)(mc / dm.n);
+        const double a00 = aa[0], a01 = aa[1], a10 = aa[2], a11 = aa[3];
+        const double u0 = v[0], u1 = v[1];
+        // traces: tr A, tr(M A) with M = Sigma0^-1 (t = 0) or Q^-1 (t >= 1)
+        const double* M = qs + ((tg == 0) ? 0 : DD);
+        double tm = M[2 + lc] * u0 + M[D + 2 + lc] * u1        // rows 0, 1 of column 2 + l
+                  + M[(2 + lc) * D] * u0 + M[(2 + lc) * D + 1] * u1;   // column 0, 1 entries A[2+l][0..1]
+        double tr = 0.0;
+#pragma unroll
         for (int k = 0; k < B; ++k) {
-            const float* rk = A + (2 + k) * D;
-            ts = fma(S0[(2 + k) * D + c], (double)rk[c], ts);
-            ts0 = fma(S0[2 + k], (double)rk[0], fma(S0[D + 2 + k], (double)rk[1], ts0));
+            const double x = v[2 + k];
+            tm = fma(M[(2 + k) * D + 2 + lc], x, tm);
+            tr = (k == lc) ? x : tr;
         }
-        if (l == 0) ts += ts0;
-    }
-
-    // LDL^T of the complement: lane c holds column c; pivot row through LDS
-    double* rb = rows[w] + sub * LPM;
-    double prod = det2;
-    int e2 = 0, neg = det2 < 0.0 ? 1 : 0;
-    bool zero = det2 == 0.0;
-#pragma unroll
-    for (int P = 0; P < B; ++P) {
-        rb[l] = col[P];
+        if (!lv) { tm = 0.0; tr = 0.0; }
+        if (l == 0) {
+            tr += a00 + a11;
+            tm += M[0] * a00 + M[1] * a10 + M[D] * a01 + M[D + 1] * a11;
+        }
+        // Schur complement column: S[k][l] = A[2+k][2+l] - u_k^T A_aa^-1 u_l
+        const double det2 = a00 * a11 - a01 * a10;
+        const double id2 = 1.0 / det2;
+        const double w0 = (a11 * u0 - a01 * u1) * id2;
+        const double w1 = (a00 * u1 - a10 * u0) * id2;
+        ub[2 * l] = u0;
+        ub[2 * l + 1] = u1;
         asm volatile("" ::: "memory");   // one wave: its LDS ops complete in issue order
-        const double piv = rb[P];
-        zero |= piv == 0.0;
-        neg ^= piv < 0.0 ? 1 : 0;
-        prod *= piv;
-        if ((P & 7) == 7 || P == B - 1) {
-            int ex;
-            prod = frexp(prod, &ex);
-            e2 += ex;
+        double col[B];
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+            const double2 uk = *(const double2*)(ub + 2 * k);
+            col[k] = (double)v[2 + k] - (uk.x * w0 + uk.y * w1);
         }
-        double ri = __builtin_amdgcn_rcp(piv);
-        ri = fma(fma(-piv, ri, 1.0), ri, ri);
-        ri = fma(fma(-piv, ri, 1.0), ri, ri);
-        const double f = col[P] * ri;
-#pragma unroll
-        for (int k = P + 1; k < B; ++k) col[k] = fma(-rb[k], f, col[k]);
         asm volatile("" ::: "memory");
-    }
-    double ld = log(fabs(prod)) + (double)e2 * 0.69314718055994530942;
-    if (zero) ld = -INFINITY;
-    else if (neg) ld = NAN;
-
-    double s_tr = lv ? tr : 0.0, s_tq = lv ? tq : 0.0, s_ts = lv ? ts : 0.0;
-    if (l == 0) {
-        s_tr += a00 + a11;
-        s_tq += tq0;
-    }
+        // LDL^T of S: lane l holds column l; pivot row through LDS
+        double prod = det2;
+        int e2 = 0, neg = det2 < 0.0 ? 1 : 0;
+        bool zero = det2 == 0.0;
 #pragma unroll
-    for (int o = 1; o < LPM; o <<= 1) {
-        s_tr += __shfl_xor(s_tr, o);
-        s_tq += __shfl_xor(s_tq, o);
-        s_ts += __shfl_xor(s_ts, o);
-    }
-    if (l == 0 && mv) {
-        double* o = a.cov_terms + mc * 4;
-        o[0] = ld;
-        o[1] = s_tr;
-        o[2] = (tg >= 1) ? s_tq : 0.0;
-        o[3] = (tg == 0) ? s_ts : 0.0;
+        for (int P = 0; P < B; ++P) {
+            rb[l] = col[P];
+            asm volatile("" ::: "memory");
+            const double piv = rb[P];
+            zero |= piv == 0.0;
+            neg ^= piv < 0.0 ? 1 : 0;
+            prod *= piv;
+            if ((P & 7) == 7 || P == B - 1) {
+                int ex;
+                prod = frexp(prod, &ex);
+                e2 += ex;
+            }
+            double ri = __builtin_amdgcn_rcp(piv);
+            ri = fma(fma(-piv, ri, 1.0), ri, ri);
+            ri = fma(fma(-piv, ri, 1.0), ri, ri);
+            const double f = col[P] * ri;
+            int k = P + 1;
+            if (k & 1) {   // to an even index, then 16-byte reads of two entries
+                col[k] = fma(-rb[k], f, col[k]);
+                ++k;
+            }
+#pragma unroll
+            for (; k + 1 < B; k += 2) {
+                const double2 r2 = *(const double2*)(rb + k);
+                col[k] = fma(-r2.x, f, col[k]);
+                col[k + 1] = fma(-r2.y, f, col[k + 1]);
+            }
+            if (k < B) col[k] = fma(-rb[k], f, col[k]);
+            asm volatile("" ::: "memory");
+            // the next group's loads fly during the second half of the
+            // elimination (half of the column is dead by then: no spills)
+            if constexpr (C::PREFETCH) {   // (clamped: the last round reloads a valid group)
+                if (P == B / 2) load(task + stride < ntask ? task + stride : task);
+            }
+        }
+        double ld = log(fabs(prod)) + (double)e2 * 0.69314718055994530942;
+        if (zero) ld = -INFINITY;
+        else if (neg) ld = NAN;
+#pragma unroll
+        for (int o = 1; o < LPM; o <<= 1) {
+            tr += __shfl_xor(tr, o);
+            tm += __shfl_xor(tm, o);
+        }
+        if (l == 0 && mv) {
+            double* o = a.cov_terms + mc * 4;
+            o[0] = ld;
+            o[1] = tr;
+            o[2] = (tg >= 1) ? tm : 0.0;
+            o[3] = (tg == 0) ? tm : 0.0;
+        }
     }
 }
 
 template <int R>
 static int launch_cov(const ame_dims* dm, const ame_cov_args* a, hipStream_t st) {
-    constexpr int per_block = (AME_NT / 64) * (64 / CovLanes<2 * R>::v);
+    using C = CovCfg<R>;
     const long long total = (long long)dm->T_local * dm->n;
-    const long long blocks = (total + per_block - 1) / per_block;
-    hipLaunchKernelGGL(ame_cov_kernel<R>, dim3((unsigned)blocks), dim3(AME_NT), 0, st, *dm, *a);
+    const long long waves = (total + C::MPW - 1) / C::MPW;
+    long long blocks = (waves + C::WPB - 1) / C::WPB;
+    // persistent grid: as many blocks as are co-resident (each wave then walks
+    // several covariance groups, prefetching the next)
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ame_cov_kernel<R>, 256, 0) == hipSuccess &&
+        cus > 0 && per_cu > 0) {
+        const long long cap = (long long)cus * per_cu;
+        if (blocks > cap) blocks = cap;
+    }
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(ame_cov_kernel<R>, dim3((unsigned)blocks), dim3(256), 0, st, *dm, *a);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
