@@ -33,7 +33,9 @@
  * the `status` word, which the host reads after the iteration.
  *
  * Layouts (row-major, fp32 unless stated):
- *   Yt      [T_local][n][n][2]    Yt[t][i][j] = Y[i][j][t0+t] of the reference
+ *   Yt      [T_local][n][ny][2]   Yt[t][i][j] = Y[i][j][t0+t] of the reference for j < n;
+ *                                 ny = n rounded up to even (rows 16-byte aligned), the
+ *                                 pad pair j = n (odd n) is zero; ame_pack_y_size()
  *   X mean  [T_local][n][d]       d = 2 + 2r, x = [a, b, U(r), V(r)]
  *   X cov   [T_local][n][d][d]
  *   consts  fp64 [5][d][d]: S0inv, Qinv, PhiT*Qinv*Phi, Qinv*Phi, PhiT*Qinv
@@ -93,7 +95,7 @@ typedef struct ame_dims {
 } ame_dims;
 
 typedef struct ame_sweep_args {
-    const float* Yt;             /* [T_local][n][n][2] */
+    const float* Yt;             /* [T_local][n][ny][2] */
     const float* x_old;          /* [T_local][n][d] means before the sweep */
     float* x_new;                /* [T_local][n][d] means after the sweep */
     const float* next_old;       /* [n][d] old means at global slice t_begin+T_local
@@ -145,7 +147,7 @@ typedef struct ame_cov_args {
 } ame_cov_args;
 
 typedef struct ame_elbo_args {
-    const float* Yt;             /* [T_local][n][n][2] */
+    const float* Yt;             /* [T_local][n][ny][2] */
     const float* x;              /* [T_local][n][d] means */
     const float* prev_final;     /* [n][d] means at global slice t_begin-1 (left halo) or NULL */
     const double* cov_terms;     /* [T_local][n][4] from ame_cov */
@@ -158,11 +160,14 @@ typedef struct ame_elbo_args {
     int32_t pairs_kernel;        /* enum ame_pairs_kernel_code (0 = default) */
 } ame_elbo_args;
 
-/* Relayout Y [n][n][T_total][2] -> Yt [T_local][n][n][2] for slices
+/* Relayout Y [n][n][T_total][2] -> Yt [T_local][n][ny][2] for slices
  * [t_begin, t_begin+T_local), and count pairs with Y[j][i] != swap(Y[i][j])
  * into *mismatch (device uint64, caller zeroes it). */
 int ame_pack_y(const float* Y, float* Yt, const ame_dims* dims,
                unsigned long long* mismatch, void* stream);
+
+/* Floats of Yt for these dims (T_local * n * ny * 2), -1 on bad dims. */
+long long ame_pack_y_size(const ame_dims* dims);
 
 /* One Gauss-Seidel sweep over all n nodes for the local slices: new means and
  * new (damped) covariances.  One workgroup per local slice; all T_local

@@ -54,7 +54,7 @@ class ame_elbo_args(ctypes.Structure):
 
 
 # every symbol include/ame_amd.h declares (checked by tests/test_capi.py)
-EXPORTS = ("ame_pack_y", "ame_sweep", "ame_sweep_kind", "ame_sweep_work_size", "ame_sweep_orders_slices", "ame_sweep_max_slices", "ame_sweep_lds_bytes", "ame_cov",
+EXPORTS = ("ame_pack_y", "ame_pack_y_size", "ame_sweep", "ame_sweep_kind", "ame_sweep_work_size", "ame_sweep_orders_slices", "ame_sweep_max_slices", "ame_sweep_lds_bytes", "ame_cov",
            "ame_elbo", "ame_elbo_work_size", "ame_elbo_pairs_diag", "ame_host_register", "ame_host_unregister",
            "ame_peer_alloc", "ame_peer_free", "ame_peer_open", "ame_peer_close",
            "ame_supported_r", "ame_last_error", "ame_version", "ame_align_work_size",
@@ -67,6 +67,8 @@ _lib = None
 def _declare(L):
     P = ctypes.POINTER
     L.ame_pack_y.argtypes = [c_vp, c_vp, P(ame_dims), c_vp, c_vp]
+    L.ame_pack_y_size.argtypes = [P(ame_dims)]
+    L.ame_pack_y_size.restype = ctypes.c_longlong
     L.ame_sweep.argtypes = [P(ame_dims), P(ame_sweep_args), c_vp]
     L.ame_sweep_max_slices.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
     L.ame_sweep_lds_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]

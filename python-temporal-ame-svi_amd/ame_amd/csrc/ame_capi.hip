@@ -237,6 +237,11 @@ long long ame_sweep_work_size(const ame_dims* dims, int kind) {
     }
 }
 
+long long ame_pack_y_size(const ame_dims* dims) {
+    if (check_dims(dims)) return -1;
+    return (long long)dims->T_local * dims->n * ame_ystride(dims->n) * 2;
+}
+
 int ame_pack_y(const float* Y, float* Yt, const ame_dims* dims, unsigned long long* mismatch,
                void* stream) {
     if (int e = check_dims(dims)) return e;

@@ -22,6 +22,11 @@ __device__ __forceinline__ double pconst_entry(const double* consts, int D, int 
     return v;
 }
 
+// Row stride (in (y0, y1) pairs) of the packed observed network Yt: n rounded up
+// to even, so every row starts 16-byte aligned (16-byte / LDS-DMA loads of any
+// row; the pad pair is zero and never used as a node).
+__host__ __device__ inline int ame_ystride(int n) { return n + (n & 1); }
+
 // Granule hand-off (cdna_hip_programming.md G16 R2): one 8-byte {epoch, value}
 // word written by ONE sc1 store; the consumer re-reads until every tag matches.
 __device__ __forceinline__ uint64_t gran_load_agent(const uint64_t* p) {

@@ -21,22 +21,27 @@
 using namespace ame;
 
 // ---------------------------------------------------------------------------
-// K0: Y [n][n][T_total][2] -> Yt [T_local][n][n][2]; count swap mismatches.
+// K0: Y [n][n][T_total][2] -> Yt [T_local][n][ny][2] (ny = ame_ystride(n), the
+// pad pair zero); count swap mismatches.
 // ---------------------------------------------------------------------------
 #if AME_PART0
 __global__ void __launch_bounds__(AME_NT)
 ame_pack_kernel(const float* __restrict__ Y, float* __restrict__ Yt, ame_dims dm,
                 unsigned long long* mismatch) {
-    const int n = dm.n, TL = dm.T_local, Tt = dm.T_total;
-    const size_t total = (size_t)TL * n * n;
+    const int n = dm.n, TL = dm.T_local, Tt = dm.T_total, ny = ame_ystride(n);
+    const size_t total = (size_t)TL * n * ny;
     unsigned long long bad = 0;
     for (size_t idx = (size_t)blockIdx.x * AME_NT + threadIdx.x; idx < total;
          idx += (size_t)gridDim.x * AME_NT) {
-        const int j = (int)(idx % n);
-        const size_t r = idx / n;
+        const int j = (int)(idx % ny);
+        const size_t r = idx / ny;
         const int i = (int)(r % n);
         const int tl = (int)(r / n);
         const int tg = dm.t_begin + tl;
+        if (j >= n) {   // pad pair
+            *(float2*)(Yt + idx * 2) = make_float2(0.f, 0.f);
+            continue;
+        }
         const float2 y = *(const float2*)(Y + (((size_t)i * n + j) * Tt + tg) * 2);
         *(float2*)(Yt + idx * 2) = y;
         if (i < j && mismatch != nullptr) {
@@ -51,7 +56,7 @@ ame_pack_kernel(const float* __restrict__ Y, float* __restrict__ Yt, ame_dims dm
 
 int ame_pack_dispatch(const float* Y, float* Yt, const ame_dims* dm, unsigned long long* mm,
                       hipStream_t st) {
-    const size_t total = (size_t)dm->T_local * dm->n * dm->n;
+    const size_t total = (size_t)dm->T_local * dm->n * ame_ystride(dm->n);
     size_t blocks = (total + AME_NT - 1) / AME_NT;
     if (blocks > 8192) blocks = 8192;
     if (blocks == 0) blocks = 1;
@@ -114,8 +119,9 @@ ame_pairs_kernel(ame_dims dm, const float* __restrict__ Yt, const float* __restr
     __shared__ float aJ[2][AME_TILE], bJ[2][AME_TILE];
     __shared__ double red[8];
 
+    const int ny = ame_ystride(n);
     const float* xs = x + (size_t)tl * n * D;
-    const float* ys = Yt + (size_t)tl * n * n * 2;
+    const float* ys = Yt + (size_t)tl * n * ny * 2;
     const float p = (float)r00, q01 = (float)r01, q10 = (float)r10, sr = (float)r11;
 
     // staging of a column tile's U, V, a, b: global loads into registers first
@@ -192,16 +198,16 @@ ame_pairs_kernel(ame_dims dm, const float* __restrict__ Yt, const float* __restr
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     const int j0 = J0 + 16 * (2 * hf + s2) + 8 * h + 2 * lq;
-                    if (irow && j0 + 2 <= n && (n & 1) == 0) {
+                    if (irow && j0 + 2 <= n) {
                         // default cache policy: non-temporal loads measured slower here
                         // (166 vs 155 us at config 3)
-                        y[s2][h] = *(const float4*)(ys + ((size_t)i * n + j0) * 2);
+                        y[s2][h] = *(const float4*)(ys + ((size_t)i * ny + j0) * 2);
                     } else {                                  // row end / odd n: per element
                         float t[4];
 #pragma unroll
                         for (int e = 0; e < 2; ++e) {
                             const bool ok = irow && j0 + e < n;
-                            const float2 v = ok ? *(const float2*)(ys + ((size_t)i * n + j0 + e) * 2)
+                            const float2 v = ok ? *(const float2*)(ys + ((size_t)i * ny + j0 + e) * 2)
                                                 : make_float2(0.f, 0.f);
                             t[2 * e] = v.x;
                             t[2 * e + 1] = v.y;
@@ -337,8 +343,9 @@ ame_pairs2_kernel(ame_dims dm, const float* __restrict__ Yt, const float* __rest
     __shared__ __attribute__((aligned(16))) char yl[4][NSLOT][P2::SLOTB];
     __shared__ double red[8];
 
+    const int ny = ame_ystride(n);   // even: every row 16-byte aligned
     const float* xs = x + (size_t)tl * n * D;
-    const float* ys = Yt + (size_t)tl * n * n * 2;
+    const float* ys = Yt + (size_t)tl * n * ny * 2;
 
     // tile sequence of this workgroup: swap mode walks strip s (J >= s) then
     // strip nb-1-s (J >= nb-1-s); otherwise strip s over all J
@@ -357,7 +364,7 @@ ame_pairs2_kernel(ame_dims dm, const float* __restrict__ Yt, const float* __rest
     for (int u = 0; u < 4; ++u) {
         yrr[u] = 4 * u + (lane >> 4);
         ygc[u] = (lane & 15) ^ yrr[u];
-        yoff[u] = (yrr[u] * n + 2 * ygc[u]) * 2;
+        yoff[u] = (yrr[u] * ny + 2 * ygc[u]) * 2;
     }
     int uoff[NUW], urow[NUW];      // staging: offset from row J0 (floats), row (>= 2^20: pad)
 #pragma unroll
@@ -383,7 +390,7 @@ ame_pairs2_kernel(ame_dims dm, const float* __restrict__ Yt, const float* __rest
         const bool real = tt < NT;
         if (real) tile(tt, I, J);
         const int c0 = J * AME_TILE + 32 * hf, r0 = I * AME_TILE + 16 * w;
-        const float* base = ys + ((size_t)r0 * n + c0) * 2;
+        const float* base = ys + ((size_t)r0 * ny + c0) * 2;
         const uint32_t dst = lds_off(&yl[w][q % NSLOT][0]);
         const bool diag = swap_mode && I == J;
         if (real && !diag && r0 + 16 <= n && c0 + 32 <= n) {
@@ -678,9 +685,10 @@ static int launch_elbo(const ame_dims* dm, const ame_elbo_args* a, hipStream_t s
     double* p2 = a->work;
     double* p3 = a->work + 2 * b2;
     if (b2 > 0) {
-        // LDS-DMA pair kernel when every Y row starts 16-byte aligned (n even);
-        // args.pairs_kernel = AME_PAIRS_V1 keeps the register-streaming kernel
-        const bool v1 = (dm->n & 1) || a->pairs_kernel == AME_PAIRS_V1;
+        // LDS-DMA pair kernel (every Yt row starts 16-byte aligned, odd n
+        // included: ame_ystride); args.pairs_kernel = AME_PAIRS_V1 keeps the
+        // register-streaming kernel
+        const bool v1 = a->pairs_kernel == AME_PAIRS_V1;
         if (v1)
             hipLaunchKernelGGL(ame_pairs_kernel<R>, dim3((unsigned)b2), dim3(AME_NT), 0, st, *dm, a->Yt,
                                a->x, a->rinv[0], a->rinv[1], a->rinv[2], a->rinv[3],

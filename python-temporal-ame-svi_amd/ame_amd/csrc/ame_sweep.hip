@@ -197,7 +197,8 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
     const float* xo = a.x_old + (size_t)t * n * D;
     const uint64_t* hand = a.hand + (size_t)t * n * D;
     uint64_t* hp = (uint64_t*)a.work + (size_t)(t * AME_GW + g) * AME_GW_RING * PW;
-    const float* ysl = a.Yt + (size_t)t * n * n * 2;
+    const int nys = ame_ystride(n);
+    const float* ysl = a.Yt + (size_t)t * n * nys * 2;
     const float r00f = (float)a.rinv[0], r01f = (float)a.rinv[1], r10f = (float)a.rinv[2], r11f = (float)a.rinv[3];
     const bool col = lane < M2;
     bool dead = false;
@@ -212,7 +213,7 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
     constexpr int YQ = (4 * AME_GW_MAXPW + AME_NT - 1) / AME_NT;
     float2 ypf[YQ];
     auto y_prefetch = [&](int m) {
-        const float2* yrow = (const float2*)(ysl + (size_t)(m < n ? m : 0) * n * 2) + base;
+        const float2* yrow = (const float2*)(ysl + (size_t)(m < n ? m : 0) * nys * 2) + base;
 #pragma unroll
         for (int u = 0; u < YQ; ++u) {
             const int e = tid + AME_NT * u;
@@ -396,7 +397,8 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     float* xn = a.x_new + (size_t)tl * n * D;
     float* cvs = a.cov + (size_t)tl * n * DD;
     float* cvw = (a.cov_new != nullptr ? a.cov_new : a.cov) + (size_t)tl * n * DD;   // damped output
-    const float* ysl = a.Yt + (size_t)tl * n * n * 2;
+    const int nys = ame_ystride(n);
+    const float* ysl = a.Yt + (size_t)tl * n * nys * 2;
     const float lr = a.lr, om = a.one_minus_lr;
     bool dead = false;
     float* Mg = MG ? (float*)a.work + (size_t)tl * n * M2 : nullptr;
@@ -508,7 +510,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     // ---- helpers ----
     float2 ypf[AME_YPF];
     auto prefetch_y = [&](int node) {   // Y row of `node` -> registers
-        const float2* yrow = (const float2*)(ysl + (size_t)node * n * 2);
+        const float2* yrow = (const float2*)(ysl + (size_t)node * nys * 2);
 #pragma unroll
         for (int r = 0; r < AME_YPF; ++r) {
             const int j = tid + AME_NT * r;
@@ -535,7 +537,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             const int j = tid + AME_NT * r;
             if (j < n) put(j, ypf[r]);
         }
-        const float2* yrow = (const float2*)(ysl + (size_t)node * n * 2);
+        const float2* yrow = (const float2*)(ysl + (size_t)node * nys * 2);
         for (int j = tid + AME_NT * AME_YPF; j < n; j += AME_NT) put(j, yrow[j]);
     };
     auto gemv = [&](int tw) {   // partial h_obs over node group (waves 1-3: tw < 192)
@@ -657,7 +659,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             float acc = 0.f;
             for (int j = node - 3; j <= node - 2; ++j) {
                 if (j < 0) continue;
-                const float2 y = *(const float2*)(ysl + ((size_t)node * n + j) * 2);
+                const float2 y = *(const float2*)(ysl + ((size_t)node * nys + j) * 2);
                 const float z0 = r00f * y.x + r01f * y.y, z1 = r10f * y.x + r11f * y.y;
                 const float* mj = mring + (j & 3) * D;
                 if (ht < R) acc = fmaf(z0, mj[2 + R + ht], acc);          // h_U += z0 V
@@ -667,7 +669,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             part[AME_GW * PW + ht] = acc;
         }
         if (ht == 0 && node >= 1) {
-            const float2 y = *(const float2*)(ysl + ((size_t)node * n + node - 1) * 2);
+            const float2 y = *(const float2*)(ysl + ((size_t)node * nys + node - 1) * 2);
             scal[40] = (double)y.x;
             scal[41] = (double)y.y;
         }

@@ -228,7 +228,8 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     float* xn = a.x_new + (size_t)tl * n * D;
     float* cvs = a.cov + (size_t)tl * n * DD;
     float* cvw = (a.cov_new != nullptr ? a.cov_new : a.cov) + (size_t)tl * n * DD;   // damped output
-    const float* ysl = a.Yt + (size_t)tl * n * n * 2;
+    const int nys = ame_ystride(n);
+    const float* ysl = a.Yt + (size_t)tl * n * nys * 2;
     // old means of slice t+1: the next local slice, or for the last local slice the
     // right rank's first slice -- next_old (gathered before the sweep), or in a
     // pipelined launch the back channel that rank fills when its slice finishes
@@ -275,7 +276,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     // ---- loader DMA pieces (whole-wave; every call issues a fixed instruction count) ----
     auto dma_y = [&](int row) {   // Y row (raw float2) -> slot row & 3 : NY instructions
         const int rw = (row < n) ? row : 0;
-        const char* base = (const char*)(ysl + (size_t)rw * n * 2);
+        const char* base = (const char*)(ysl + (size_t)rw * nys * 2);
         const uint32_t dst = lds_off(yring + (size_t)(row & 3) * YS);
         for (int q = 0; q < NY; ++q) {
             int off = (q * 64 + lane) * 16;
@@ -498,7 +499,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         // Y rows 0 and 1 into ring slots 0 and 1 (plain loads)
         for (int e = hl; e < 2 * n; e += kNH) {
             const int rw = e / n, j = e - rw * n;
-            yring[(size_t)rw * YS + j] = (rw < n) ? *(const float2*)(ysl + ((size_t)rw * n + j) * 2)
+            yring[(size_t)rw * YS + j] = (rw < n) ? *(const float2*)(ysl + ((size_t)rw * nys + j) * 2)
                                                     : make_float2(0.f, 0.f);
         }
     }

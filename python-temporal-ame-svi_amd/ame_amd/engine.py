@@ -3,7 +3,8 @@
 One engine per process / GPU.  It owns, for the local time slices
 [t_begin, t_begin + T_local):
 
-    Yt        [T_local][n][n][2] fp32   observed network, time-major (ame_pack_y)
+    Yt        [T_local][n][ny][2] fp32  observed network, time-major, rows padded to
+                                        even length (ame_pack_y)
     xs[k]     [T_local][n][d]    fp32   means: ring of spec_depth + 1 states
     covs[k]   [T_local][n][d][d] fp32   covariances: same ring (x_a / cov = current)
     hand      [T_local][n][d]    u64    lane-to-lane {epoch,value} granules
@@ -353,7 +354,11 @@ class DeviceEngine:
         if src.dtype != torch.float32:
             src = src.float()
         src = src.to(self.dev).contiguous()
-        self.Yt = torch.empty(sh.T_local, self.n, self.n, 2, dtype=torch.float32, device=self.dev)
+        ysz = int(self.L.ame_pack_y_size(ctypes.byref(self.dims)))
+        if ysz < 0:
+            _lib.check(-1, "ame_pack_y_size")
+        self.ny = ysz // (2 * sh.T_local * self.n)   # row stride: n rounded up to even
+        self.Yt = torch.empty(sh.T_local, self.n, self.ny, 2, dtype=torch.float32, device=self.dev)
         mm = torch.zeros(1, dtype=torch.int64, device=self.dev)
         rc = self.L.ame_pack_y(_ptr(src), _ptr(self.Yt), ctypes.byref(self.dims), _ptr(mm),
                                self._sp())
@@ -400,7 +405,7 @@ class DeviceEngine:
         for g, (off, size) in enumerate(self.groups):
             def at(t, slices, per_slice, esize):   # pointer to local slice `slices` of t
                 return ctypes.c_void_p(t.data_ptr() + slices * per_slice * esize)
-            nd, ndd, nn2 = n * d, n * d * d, n * n * 2
+            nd, ndd, nn2 = n * d, n * d * d, n * self.ny * 2
             g_halo_in = halo_in if g == 0 else at(self.hand, off - 1, nd, 8)
             g_halo_out = halo_out if g == last else None
             g_next_old = next_old if g == last else at(self.xs[src], off + size, nd, 4)

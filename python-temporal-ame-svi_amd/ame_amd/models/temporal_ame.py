@@ -99,24 +99,39 @@ class TemporalAMEModel:
     # ------------------------------------------------------------------
     # generators
     # ------------------------------------------------------------------
-    def generate_data(self, return_latents: bool = False):
-        """Reference-identical generator (temporal_ame.py:147-220)."""
+    def generate_data(self, return_latents: bool = False, X: Optional[torch.Tensor] = None):
+        """Reference-identical generator (temporal_ame.py:147-220).
+
+        ``X`` (optional, (n, T, d)): take these latent trajectories instead of
+        forming them, while consuming exactly the random draws the reference
+        spends on them.  The reference forms X with small MKL matvecs whose
+        rounding depends on the host CPU's code path; given X, the observations
+        below are bit-identical on any host (tests/test_reference_c2.py checks
+        both against the reference's own run)."""
         n, T, d = self.n, self.T, self.d
-        self.X = torch.zeros(n, T, d)
         self.Y = torch.zeros(n, n, T, 2)
         L0 = MultivariateNormal(torch.zeros(d), self.sigma0())._unbroadcasted_scale_tril
         LQ = MultivariateNormal(torch.zeros(d), self.Q)._unbroadcasted_scale_tril
         LR = MultivariateNormal(torch.zeros(2), self.R)._unbroadcasted_scale_tril
-        z_d, z_2 = torch.zeros(d), torch.zeros(2)
+        z_d = torch.zeros(d)
 
         def sample(L, loc, k):   # MultivariateNormal.rsample with one normal_() draw
             eps = torch.empty(k).normal_()
             return loc + torch.matmul(L, eps.unsqueeze(-1)).squeeze(-1)
 
-        for i in range(n):
-            self.X[i, 0] = sample(L0, z_d, d)
-            for t in range(1, T):
-                self.X[i, t] = torch.matmul(self.Phi, self.X[i, t - 1]) + sample(LQ, z_d, d)
+        if X is None:
+            self.X = torch.zeros(n, T, d)
+            for i in range(n):
+                self.X[i, 0] = sample(L0, z_d, d)
+                for t in range(1, T):
+                    self.X[i, t] = torch.matmul(self.Phi, self.X[i, t - 1]) + sample(LQ, z_d, d)
+        else:
+            self.X = torch.as_tensor(X, dtype=torch.float32).clone()
+            if tuple(self.X.shape) != (n, T, d):
+                raise ValueError(f"X has shape {tuple(self.X.shape)}, expected {(n, T, d)}")
+            scratch = torch.empty(d)
+            for _ in range(n * T):   # the same draws, in the same order
+                scratch.normal_()
         # Observation noise (temporal_ame.py:203-214): one 2-vector draw per
         # upper-triangle dyad, t-major then i then j.  A CPU normal_() call on
         # fewer than 16 floats takes the scalar Box-Muller path, which caches the
@@ -136,7 +151,7 @@ class TemporalAMEModel:
             p0 = (l00 * e[:, 0]).float()
             p10 = (l10 * e[:, 0]).float()
             p1 = (l11 * e[:, 1] + p10.double()).float()
-            mu_t = self.compute_mean(self.X[:, t, :2], self.X[:, t, 2:])
+            mu_t = self._mean_seqfma(self.X[:, t, :2], self.X[:, t, 2:])
             dy = mu_t[iu[0], iu[1]] + torch.stack([p0, p1], dim=1)
             self.Y[iu[0], iu[1], t] = dy
             self.Y[iu[1], iu[0], t, 0] = dy[:, 1]
@@ -144,6 +159,23 @@ class TemporalAMEModel:
         if return_latents:
             return self.Y, self.X
         return self.Y
+
+    def _mean_seqfma(self, A: torch.Tensor, M: torch.Tensor) -> torch.Tensor:
+        """compute_mean (static_ame.py:189-238) of one slice with U V^T summed as
+        the reference's fp32 sgemm sums it on the fixture host (MKL: one fused
+        multiply-add per k, k ascending; measured bit-exact), but independent of
+        the host's BLAS: each step is an exact fp64 product plus the running fp32
+        sum, rounded once to fp32."""
+        a, b = A[:, 0], A[:, 1]
+        U, V = M[:, :self.r].double(), M[:, self.r:].double()
+        mult = torch.zeros(A.shape[0], A.shape[0], dtype=torch.float32)
+        for k in range(self.r):
+            mult = (torch.outer(U[:, k], V[:, k]) + mult.double()).float()
+        additive = a.unsqueeze(1) + b.unsqueeze(0)
+        mu = torch.zeros(A.shape[0], A.shape[0], 2)
+        mu[:, :, 0] = additive + mult
+        mu[:, :, 1] = additive.t() + mult.t()
+        return mu
 
     def generate_data_fast(self, return_latents: bool = False, device=None,
                            seed: Optional[int] = None):

@@ -10,10 +10,17 @@ checks the digest before comparing.  Per (method, dtype) run it stores the
 ELBO / MSE trajectories of 2 fit() iterations, the ELBO split after each, and
 sampled X_mean rows / X_cov blocks after each iteration.
 
+The reference's X (the latent trajectories, 1.2 MB) IS committed: X comes from
+small MKL matvecs whose rounding depends on the host CPU's MKL code path (the
+GPU box's EPYC rounds differently from this Xeon), while Y given X is
+reproducible anywhere (ame_amd's generator forms U V^T with the sequential-FMA
+order MKL's sgemm uses here, and the noise stream exactly).
+
 Usage (from the repo root; one process per run, ~10 min each)::
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_c2.py good f32
     ...
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_c2.py --x     # X only
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_c2.py --merge
 
 Reference call sites (file:line under /root/reference):
@@ -84,6 +91,22 @@ def run(method, prec):
     print(f"{method} {prec}: elbo {rec['elbo']} recon {rec['recon']}", flush=True)
 
 
+def save_x():
+    """The reference's latent trajectories X (generate_data), for the GPU box."""
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, REF)
+    import numpy as np
+    import torch
+    torch.set_num_threads(1)
+    from src.models import TemporalAMEModel
+    m = TemporalAMEModel(n_nodes=N, n_time=T, latent_dim=R, ar_coefficient=0.8,
+                         rho_dyadic=0.5, seed=42)
+    Y, X = m.generate_data(return_latents=True)
+    os.makedirs(PARTS, exist_ok=True)
+    np.savez(os.path.join(PARTS, "X.npz"), X=X.numpy(), X_sha256=np.array(sha(X.numpy())),
+             Y_sha256=np.array(sha(Y.numpy())))
+
+
 def merge():
     import numpy as np
     out = {"nodes": np.array(NODES, dtype=np.int64), "cov_it": np.array(COV_IT, dtype=np.int64),
@@ -91,6 +114,11 @@ def merge():
     shas = set()
     for f in sorted(os.listdir(PARTS)):
         if not f.endswith(".npz"):
+            continue
+        if f == "X.npz":
+            zx = np.load(os.path.join(PARTS, f))
+            out["X_true"] = zx["X"]
+            shas.add((str(zx["Y_sha256"]), str(zx["X_sha256"])))
             continue
         key = f[:-4]
         z = np.load(os.path.join(PARTS, f))
@@ -109,5 +137,7 @@ def merge():
 if __name__ == "__main__":
     if sys.argv[1:] == ["--merge"]:
         merge()
+    elif sys.argv[1:] == ["--x"]:
+        save_x()
     else:
         run(sys.argv[1], sys.argv[2])

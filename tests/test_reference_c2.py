@@ -2,7 +2,10 @@
 (tests/golden/c2_reference.npz, written by tests/golden/make_golden_c2.py):
 
 * ame_amd's reference-stream generator rebuilds the reference's Y and X bit
-  for bit (SHA-256; temporal_ame.py:147-220);
+  for bit (SHA-256; temporal_ame.py:147-220) -- X here, where the fixture was
+  made (X's small MKL matvecs round by the host's MKL code path), and Y from the
+  reference's X (the fixture's X_true) on any host, which is what the GPU test
+  (tests/test_gpu_reference_c2.py) uses on the GPU box;
 * the VI classes draw the reference's initial state (digests;
   structured_mf.py:74-113, naive_mf.py:71-87) -- host code, no GPU;
 * the fp64 oracle (oracle/ame_oracle.py) follows the reference's fp64
@@ -27,13 +30,16 @@ def _sha(a):
 
 @pytest.fixture(scope="module")
 def c2():
+    """The config-2 model with Y regenerated from the reference's X."""
     if not os.path.exists(FIX):
         pytest.skip("c2_reference.npz not generated")
+    import torch
     from ame_amd import TemporalAMEModel
     z = np.load(FIX)
     n, T, r = int(z["n"]), int(z["T"]), int(z["r"])
+    assert _sha(z["X_true"]) == str(z["X_sha256"])
     m = TemporalAMEModel(n, T, r, ar_coefficient=0.8, rho_dyadic=0.5, seed=42)
-    Y, X = m.generate_data(return_latents=True)
+    Y, X = m.generate_data(return_latents=True, X=torch.from_numpy(z["X_true"]))
     return z, m, _sha(Y.numpy()), _sha(X.numpy())
 
 
@@ -42,6 +48,19 @@ def test_reference_stream_regenerated(c2):
     assert xsha == str(z["X_sha256"])
     assert ysha == str(z["Y_sha256"])
     assert np.array_equal(m.Y.numpy()[z["nodes"]][:, :8], z["Y_rows"])
+
+
+def test_reference_stream_from_seed_alone():
+    """Without the reference's X: X (and so Y) from the seed, on this host."""
+    if not os.path.exists(FIX):
+        pytest.skip("c2_reference.npz not generated")
+    from ame_amd import TemporalAMEModel
+    z = np.load(FIX)
+    m = TemporalAMEModel(int(z["n"]), int(z["T"]), int(z["r"]), ar_coefficient=0.8,
+                         rho_dyadic=0.5, seed=42)
+    Y, X = m.generate_data(return_latents=True)
+    assert _sha(X.numpy()) == str(z["X_sha256"])
+    assert _sha(Y.numpy()) == str(z["Y_sha256"])
 
 
 @pytest.mark.parametrize("method", ["good", "bad", "naive"])
