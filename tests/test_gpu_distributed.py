@@ -1,9 +1,17 @@
 """Time-sharded sweep on the GPU: 2-4 ranks (processes) on one MI355X, boundary
-means handed over through the host-mapped granule buffers while the ranks'
-sweep kernels run (with 3+ ranks a middle rank has both neighbours: left halo
-in, right halo out and both back channels at once; 6 iterations keep sweeps
-queued two deep across ranks).  Must reproduce the single-process result bit for bit (means,
-covariances) and the ELBO/MSE to fp64 round-off."""
+means handed over through peer buffers (fine-grained device memory exported
+with an IPC handle, ame_peer_alloc / ame_peer_open) while the ranks' sweep
+kernels run; with 3+ ranks a middle rank has both neighbours (left halo in,
+right halo out and both back channels at once).  Pipelined sweeps are queued
+spec_depth deep on every rank (derived from the global slice count by
+DeviceEngine, DESIGN.md §5, or given explicitly).  Must reproduce the
+single-process result bit for bit (means, covariances) and the ELBO/MSE to fp64
+round-off.
+
+Only the same-device IPC path runs here (one GPU per box): the ranks' peer
+buffers live on one device.  The cross-device xGMI path (a neighbour's buffer on
+another GPU) is the same code with the handle opened on another device; it has
+not run on hardware in this repository's tests."""
 import os
 import socket
 
@@ -24,16 +32,21 @@ def _free_port():
     return p
 
 
-def _run(n, T, r, method, lr, iters, distributed):
+def _run(n, T, r, method, lr, iters, distributed, depth=None):
     from ame_amd import TemporalAMEModel, TemporalAMENaiveMFVI, TemporalAMEStructuredMFVI
     m = TemporalAMEModel(n, T, r, seed=21)
     m.generate_data_fast(seed=4)
     dev = torch.device("cuda", 0)
+    opts = {} if depth is None else {"spec_depth": depth}
     if method == "naive":
-        vi = TemporalAMENaiveMFVI(m, learning_rate=lr, device=dev, distributed=distributed)
+        vi = TemporalAMENaiveMFVI(m, learning_rate=lr, device=dev, distributed=distributed,
+                                  engine_options=opts)
     else:
         vi = TemporalAMEStructuredMFVI(m, factorization=method, learning_rate=lr, device=dev,
-                                       distributed=distributed)
+                                       distributed=distributed, engine_options=opts)
+    eng = vi.engine
+    if distributed and depth is not None:
+        assert eng.pipelined and eng.spec_depth == depth and len(eng.xs) == depth + 1
     h = vi.fit(max_iter=iters, tolerance=0.0, verbose=False)
     return (vi.X_mean.numpy().copy(), vi.X_cov.numpy().copy(),
             [float(e) for e in h["elbo"]], list(h["reconstruction_error"]))
@@ -43,20 +56,25 @@ def _worker(rank, world, port, args, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        out = _run(*args, distributed=True)
+        n, T, r, method, lr, iters, depth = args
+        out = _run(n, T, r, method, lr, iters, True, depth)
         if rank == 0:
             q.put(out)
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n,T,r,method,lr,iters", [
-    (2, 64, 8, 4, "good", 0.5, 3), (2, 40, 6, 3, "bad", 1.0, 3), (2, 48, 5, 2, "naive", 0.3, 3),
-    (3, 50, 9, 3, "good", 0.5, 6), (4, 40, 12, 4, "good", 0.7, 6)])
-def test_ranks_one_gpu(world, n, T, r, method, lr, iters):
+@pytest.mark.parametrize("world,n,T,r,method,lr,iters,depth", [
+    (2, 64, 8, 4, "good", 0.5, 3, None), (2, 40, 6, 3, "bad", 1.0, 3, None),
+    (2, 48, 5, 2, "naive", 0.3, 3, None), (3, 50, 9, 3, "good", 0.5, 6, None),
+    (4, 40, 12, 4, "good", 0.7, 6, None),
+    # the queue depth the model gives at N = 8: 3 sweeps ahead
+    # on 3 and 4 ranks, 8 iterations (several wraps of the state ring)
+    (3, 60, 12, 4, "good", 0.5, 8, 3), (4, 64, 16, 3, "bad", 0.8, 8, 3)])
+def test_ranks_one_gpu(world, n, T, r, method, lr, iters, depth):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    args = (n, T, r, method, lr, iters)
+    args = (n, T, r, method, lr, iters, depth)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -76,7 +94,8 @@ def test_ranks_one_gpu(world, n, T, r, method, lr, iters):
             p.join()
     assert codes == [0] * world, f"rank exit codes {codes}"
     mean_d, cov_d, elbo_d, rec_d = result
-    mean_s, cov_s, elbo_s, rec_s = _run(*args, distributed=False)
+    n, T, r, method, lr, iters, _ = args
+    mean_s, cov_s, elbo_s, rec_s = _run(n, T, r, method, lr, iters, False)
     assert np.array_equal(mean_d, mean_s)
     assert np.array_equal(cov_d, cov_s)
     assert np.allclose(elbo_d, elbo_s, rtol=1e-6, atol=0)

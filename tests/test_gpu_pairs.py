@@ -1,9 +1,10 @@
 """ELBO pair kernel v2 (LDS-DMA Y stream, ame_elbo.hip ame_pairs2_kernel)
-against the register-streaming v1 kernel and the fp64 oracle.
+against the register-streaming v1 kernel and the fp64 oracle, at even and
+odd n (Yt rows are padded to even length, so v2 runs at any n).
 
 Reference: structured_mf.py:124-150 (expected log-likelihood),
-temporal_ame.py:255-291 (reconstruction error).  v2 runs whenever n is even;
-engine option pairs_kernel=AME_PAIRS_V1 selects v1.  Both form the same fp32 products and per-tile fp32
+temporal_ame.py:255-291 (reconstruction error).  v2 is the default at every
+n; engine option pairs_kernel=AME_PAIRS_V1 selects v1.  Both form the same fp32 products and per-tile fp32
 partial sums, so they agree to a few fp32 ulps of the total (bound 1e-6
 relative, stated here); against the fp64 oracle the ELBO log-likelihood and
 the reconstruction error are held to 5e-6 relative, as in test_gpu_parity.py.
@@ -28,7 +29,10 @@ def _sums(vi, v1):
 @pytest.mark.parametrize("n,T,r,swap", [
     (64, 3, 16, True), (130, 2, 16, True), (200, 3, 8, False), (256, 4, 32, True),
     (1024, 8, 16, True), (1024, 2, 16, False), (2, 3, 1, True), (98, 2, 5, True),
-    (192, 5, 3, False), (4096, 1, 32, True)])
+    (192, 5, 3, False), (4096, 1, 32, True),
+    # odd n: rows padded to even length (ame_ystride), the v2 kernel's DMA
+    # chunks stay 16-byte aligned and the pad column is masked
+    (97, 3, 5, True), (257, 2, 16, False), (1023, 2, 16, True), (3, 2, 2, True)])
 def test_pairs_v2_matches_v1_and_oracle(n, T, r, swap, gpu_device):
     import ame_oracle as O
     from ame_amd import TemporalAMEModel, TemporalAMEStructuredMFVI
