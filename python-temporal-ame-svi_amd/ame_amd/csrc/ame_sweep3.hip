@@ -137,8 +137,8 @@ struct Lay {
     static constexpr int oMu64 = al16(oRec + 8 * 2 * D * 8);       // [par][k] new mean (fp64)
     static constexpr int oMu32 = al16(oMu64 + 8 * 2 * D);          // [par][k] new mean (fp32)
     static constexpr int oG = al16(oMu32 + 4 * 2 * D);             // [node&1][k] g of node
-    static constexpr int oJn = al16(oG + 8 * 2 * D);               // [q][k] J rows of node i+2 (old)
-    static constexpr int oV = al16(oJn + 8 * 2 * D);               // [node&1][k]{v, yv0, yv1, vA}
+    static constexpr int oJn = al16(oG + 8 * 2 * D);               // [node&1][q][k] J rows of node i+2 (old)
+    static constexpr int oV = al16(oJn + 8 * 4 * D);               // [node&1][k]{v, yv0, yv1, vA}
     static constexpr int oDots = al16(oV + 8 * 2 * D * 4);         // HX results
     static constexpr int oRed = al16(oDots + 8 * 32);              // solver reduction gather
     static constexpr int oGP = al16(oRed + 8 * 64);                // [node&1][wave][k] GEMV partials
@@ -620,12 +620,15 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         }
         if (k < D && p == 0) g64[(m & 1) * D + k] = g;
     };
-    auto jn_fill = [&](int node) {   // J rows of `node` (old) -> jn64; lanes < D of the calling wave
+    // J rows of `node` (old) -> jn64 slot node & 1 (lanes < D of the calling wave).
+    // Double-buffered: hw 0 fills node i+2 during step i while the solver may
+    // still be reading node i+1's (its prologue prep of step 0 overlaps step 0)
+    auto jn_fill = [&](int node) {
         if (lane < D) {
             double j0, j1;
             jcol<R>(xring + (node & 7) * 64, node < n, lane, j0, j1);
-            jn64[lane] = j0;
-            jn64[D + lane] = j1;
+            jn64[(node & 1) * 2 * D + lane] = j0;
+            jn64[(node & 1) * 2 * D + D + lane] = j1;
         }
     };
 
@@ -692,24 +695,25 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         // Runs at the end of the previous step, after the solver's own work.
         double v = 0, yv0 = 0, yv1 = 0, vA = 0, nq0 = 0, nq1 = 0;
         auto prep = [&](int node) {
+            const double* jn = jn64 + ((node + 1) & 1) * 2 * D;   // J rows of node + 1
             if (!kl) return;
             const double* gg = g64 + (node & 1) * D;
             double s0 = 0, s1 = 0, s2 = 0, t0 = 0, t1 = 0, t2 = 0;
 #pragma unroll
             for (int c = 0; c < D; c += 2) {
                 s0 = fma(brow[c], gg[c], s0);
-                s1 = fma(brow[c], jn64[c], s1);
-                s2 = fma(brow[c], jn64[D + c], s2);
+                s1 = fma(brow[c], jn[c], s1);
+                s2 = fma(brow[c], jn[D + c], s2);
                 t0 = fma(brow[c + 1], gg[c + 1], t0);
-                t1 = fma(brow[c + 1], jn64[c + 1], t1);
-                t2 = fma(brow[c + 1], jn64[D + c + 1], t2);
+                t1 = fma(brow[c + 1], jn[c + 1], t1);
+                t2 = fma(brow[c + 1], jn[D + c + 1], t2);
             }
             v = s0 + t0;
             yv0 = s1 + t1;
             yv1 = s2 + t2;
             vA = brow[0] * gg[0] + brow[1] * gg[1];
-            nq0 = jn64[k];
-            nq1 = jn64[D + k];
+            nq0 = jn[k];
+            nq1 = jn[D + k];
         };
         prep(0);
         double Wp0 = 0, Wp1 = 0, Xp0 = 0, Xp1 = 0, Lp0 = 0, Lp1 = 0, Gp0 = 0, Gp1 = 0;

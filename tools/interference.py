@@ -23,7 +23,6 @@ def _unsplit_sources():
     from ame_amd.build import UNSPLIT_SOURCES
     return UNSPLIT_SOURCES
 
-SRCS = _unsplit_sources()
 
 
 def build(tag, defs):
@@ -31,7 +30,7 @@ def build(tag, defs):
     csrc = os.path.join(PKG, "ame_amd", "csrc")
     objs = []
     procs = []
-    for src in SRCS:
+    for src in _unsplit_sources():
         o = os.path.join(BDIR, src.replace(".hip", f"_var{tag}.o"))
         procs.append(subprocess.Popen(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17",
                                        "-DAME_ONLY_R=16", *[f"-D{d}" for d in defs if d], "-Wno-pass-failed",

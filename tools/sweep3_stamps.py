@@ -24,14 +24,13 @@ def _unsplit_sources():
     from ame_amd.build import UNSPLIT_SOURCES
     return UNSPLIT_SOURCES
 
-SRCS = _unsplit_sources()
 NAMES = {
     0: ["start", "J+kj", "reduce", "ddone", "2x2+assembly", "publish", "kcnt", "brow", "gcnt", "prep(v,yv)"],
     1: ["start", "pring", "poll", "hf1", "HB", "GEMV", "spin", "-", "-", "end"],
     2: ["start", "HX", "-", "-", "HB", "GEMV", "-", "-", "-", "end"],
     3: ["start", "-", "-", "-", "(no HB)", "GEMV", "DMA", "-", "-", "vmwait"],
 }
-WAVES = ["solver(w0)", "hw0(w1)", "hw5(w6)", "hw6(w7)"]
+WAVES = ["solver(w0)", "hw0(w1)", "hw5(w6)", "hw6(w7)"]   # the kernel stamps waves 0, 1, 6, 7
 
 
 def build(r=16):
@@ -40,7 +39,7 @@ def build(r=16):
     defs = [f"-D{d}" for d in (" ".join(a for a in sys.argv if a.startswith("--defs=")).replace(
         "--defs=", "")).split(",") if d]
     objs = []
-    for src in SRCS:
+    for src in _unsplit_sources():
         o = os.path.join(BDIR, src.replace(".hip", f"_s3{TAG}.o"))
         subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC",
                                "-std=c++17", "-DAME_STAMPS", f"-DAME_ONLY_R={r}", *defs,

@@ -12,10 +12,9 @@ def _unsplit_sources():
     from ame_amd.build import UNSPLIT_SOURCES
     return UNSPLIT_SOURCES
 
-SRCS = _unsplit_sources()
 if "--build" in sys.argv:
     objs = []
-    for src in SRCS:
+    for src in _unsplit_sources():
         o = os.path.join(BDIR, src.replace(".hip", "_wd.o"))
         subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17",
                                "-DAME_WDEBUG", "-DAME_ONLY_R=32", "-Wno-pass-failed", "-c",
