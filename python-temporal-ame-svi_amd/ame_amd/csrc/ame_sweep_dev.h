@@ -1,5 +1,5 @@
-// Device helpers shared by the latency-optimised sweep kernels (ame_sweep3.hip,
-// ame_sweep4.hip): workgroup-local hand-off counters in LDS, LDS-DMA
+// Device helpers of the LDS-DMA kernels (ame_sweep3.hip, ame_sweep.hip,
+// ame_elbo.hip): workgroup-local hand-off counters in LDS, LDS-DMA
 // (global_load_lds) issue wrappers with manual vmcnt accounting, the packed
 // triangle index decode, the J entries of a node and two DPP pair-adds.
 #pragma once
@@ -65,7 +65,7 @@ __device__ __forceinline__ void dma16_sys(const void* gsrc, uint32_t lds) {
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc0 sc1\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
 }
-__device__ __forceinline__ void dma4_sys(const void* gsrc, uint32_t lds) {   // host-mapped source
+__device__ __forceinline__ void dma4_sys(const void* gsrc, uint32_t lds) {   // system-coherent (peer) source
     uint32_t keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off sc0 sc1\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
