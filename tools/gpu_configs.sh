@@ -16,4 +16,4 @@ run() {
 run --steps 30 --warmup 3 --n 256 --t-per-gpu 64 --latent-dim 8
 run --steps 30 --warmup 3 --n 1024 --t-per-gpu 64 --latent-dim 16
 for V in naive bad; do run --steps 30 --warmup 3 --variant $V; done
-for V in naive good bad; do run --steps 3 --warmup 1 --n 4096 --t-per-gpu 32 --latent-dim 32 --variant $V; done
+for V in naive good bad; do run --steps 10 --warmup 2 --n 4096 --t-per-gpu 32 --latent-dim 32 --variant $V; done
