@@ -50,13 +50,13 @@ using namespace ame;
 #ifdef AME_STAMPS
 // Diagnostic build only (cdna_hip_programming.md §7, in-kernel stamps): the
 // middle lane records s_memtime at marked points of steps [S3_I0, S3_I0+16) for
-// waves 0 (solver), 1 (hw 0), 4 (hw 3) and 7 (hw 6); every lane records
+// every wave (0 = solver, w = helper wave w-1); every lane records
 // s_memrealtime when it reaches steps 0, n/4, n/2, 3n/4 and n.
 #define S3_I0 256
-__device__ unsigned long long g_s3_stamps[4 * 16 * 16];
+__device__ unsigned long long g_s3_stamps[8 * 16 * 16];
 __device__ unsigned long long g_s3_prog[256 * 5];
 __device__ unsigned int g_s3_hwid[8];
-#define S3W(w) ((w) == 0 ? 0 : (w) == 1 ? 1 : (w) == 6 ? 2 : (w) == 7 ? 3 : -1)
+#define S3W(w) (w)
 #define STAMP3(slot)                                                                           \
     do {                                                                                       \
         if (tl == TL / 2 && lane == 0 && i >= S3_I0 && i < S3_I0 + 16 && S3W(wave) >= 0) {     \
@@ -514,7 +514,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
 
     // GEMV of node m over nodes j (excluding j in {m-2, m-1, m}) from raw Y values
     // ysrc[j]; stashes y_{m,m-1}, y_{m,m-2}; partials -> gp[m&1][hw][.]
-    auto gemv = [&](int m, const float2* ysrc) {
+    auto gemv = [&](int m, const float2* ysrc, int i) {   // i: the step (stamps only)
         float acc[D];
 #pragma unroll
         for (int c = 0; c < D; ++c) acc[c] = 0.f;
@@ -565,12 +565,14 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 }
             }
         }
+        STAMP3(7);
         int idx;
 #ifndef AME_ABL_GEMV_NORED
         const float v = wave_reduce_scatter<D>(acc, lane, idx);
 #else
         const float v = acc[lane % D]; idx = lane;
 #endif
+        STAMP3(8);
         if (idx < D) gp[((m & 1) * 7 + hw) * D + idx] = v;
         // raw y_{m,m-1}, y_{m,m-2} for the solver / HF1 (owner lanes only)
         const int jm1 = m - 1, jm2 = m - 2;
@@ -634,8 +636,8 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
 
     // ---- prologue work: g_0, GEMV partials of node 1, v_0 / yv_0; rings for steps 0..2 ----
     if (wave >= 1) {
-        gemv(0, yring);
-        gemv(1, yring + YS);
+        gemv(0, yring, -1);
+        gemv(1, yring + YS, -1);
         if (hw <= 2) {
             uint64_t g0 = 0;
             if (tg > 0 && lane < D)
@@ -1031,9 +1033,9 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 }
                 // HE: GEMV of node i+2 (its Y row landed in the ring by step i-1)
 #ifdef AME_ABL_NOGEMV012
-                if (i + 2 < n && hw >= 3) gemv(i + 2, yring + (size_t)((i + 2) & 3) * YS);
+                if (i + 2 < n && hw >= 3) gemv(i + 2, yring + (size_t)((i + 2) & 3) * YS, i);
 #else
-                if (i + 2 < n) gemv(i + 2, yring + (size_t)((i + 2) & 3) * YS);
+                if (i + 2 < n) gemv(i + 2, yring + (size_t)((i + 2) & 3) * YS, i);
 #endif
                 STAMP3(5);
                 // loader: this step's batch -- Y row i+5, covariance of node i+2, old

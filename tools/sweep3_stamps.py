@@ -1,7 +1,8 @@
 """Diagnostic for the v3 sweep (ame_sweep3.hip): in-kernel s_memtime stamps.
 
     python tools/sweep3_stamps.py --build      # here: hipcc -DAME_STAMPS -> _build/libame_amd_stamps3.so
-    python tools/sweep3_stamps.py              # GPU box: config-3 sweeps, print per-wave timelines
+    python tools/sweep3_stamps.py [--tag=T] [--iters=K]   # GPU box: config-3 fit, per-wave timelines
+                                               # of the last sweep (K > 2: a pipelined steady-state one)
 
 The stamped build's run time is never quoted; only its shares / timelines.
 """
@@ -24,13 +25,21 @@ def _unsplit_sources():
     from ame_amd.build import UNSPLIT_SOURCES
     return UNSPLIT_SOURCES
 
-NAMES = {
+NAMES = {   # stamp slot names per wave (the kernel stamps every wave; see ame_sweep3.hip STAMP3)
     0: ["start", "J+kj", "reduce", "ddone", "2x2+assembly", "publish", "kcnt", "brow", "gcnt", "prep(v,yv)"],
-    1: ["start", "pring", "poll", "hf1", "HB", "GEMV", "spin", "-", "-", "end"],
-    2: ["start", "HX", "-", "-", "HB", "GEMV", "-", "-", "-", "end"],
-    3: ["start", "-", "-", "-", "(no HB)", "GEMV", "DMA", "-", "-", "vmwait"],
 }
-WAVES = ["solver(w0)", "hw0(w1)", "hw5(w6)", "hw6(w7)"]   # the kernel stamps waves 0, 1, 6, 7
+for _w in range(1, 8):
+    _hw = _w - 1
+    NAMES[_w] = ["start",
+                 "HX" if _hw == 5 else ("pring" if _hw <= 2 else "-"),
+                 "poll" if _hw <= 2 else "-",
+                 "hf1" if _hw <= 2 else "-",
+                 "HB" if _hw <= 5 else "(no HB)",
+                 "GEMV",
+                 "DMA" if _hw == 6 else ("spin" if _hw <= 2 else "-"),
+                 "gemv-fma", "gemv-rs",
+                 "vmwait" if _hw == 6 else "end"]
+WAVES = ["solver(w0)"] + [f"hw{w - 1}(w{w})" for w in range(1, 8)]
 
 
 def build(r=16):
@@ -60,14 +69,15 @@ def run():
     m = TemporalAMEModel(1024, 128, 16, seed=42)
     m.generate_data_fast(device=dev)
     vi = TemporalAMEStructuredMFVI(m, factorization="good", learning_rate=0.01, device=dev)
-    vi.fit(max_iter=2, tolerance=0.0, verbose=False)
+    iters = int(([a.split("=", 1)[1] for a in sys.argv if a.startswith("--iters=")] or ["2"])[0])
+    vi.fit(max_iter=iters, tolerance=0.0, verbose=False)   # stamps: the last sweep that ran
     torch.cuda.synchronize()
     L = _lib.lib()
     L.ame_debug_read_stamps3.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-    st = np.zeros(4 * 16 * 16, dtype=np.uint64)
+    st = np.zeros(8 * 16 * 16, dtype=np.uint64)
     pg = np.zeros(256 * 5, dtype=np.uint64)
     assert L.ame_debug_read_stamps3(st.ctypes.data, pg.ctypes.data) == 0
-    st = st.reshape(4, 16, 16).astype(np.int64)
+    st = st.reshape(8, 16, 16).astype(np.int64)
     L.ame_debug_read_hwid3.argtypes = [ctypes.c_void_p]
     hw = np.zeros(8, dtype=np.uint32)
     L.ame_debug_read_hwid3(hw.ctypes.data)
@@ -76,7 +86,7 @@ def run():
     pg = pg.reshape(256, 5).astype(np.int64)[:128]
     t0 = st[0, :, 0].min()
     print("step period (solver start-to-start), cycles:", np.diff(st[0, :, 0])[:15].tolist())
-    for w in range(4):
+    for w in range(8):
         print(f"--- {WAVES[w]} (cycles after solver step start, median over 16 steps)")
         rel = st[w] - st[0, :, 0][:, None]
         for sl, nm in enumerate(NAMES[w]):
