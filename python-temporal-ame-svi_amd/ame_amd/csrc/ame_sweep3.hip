@@ -16,7 +16,8 @@
 //    lane t-1 hands mu_{i,t-1}^new to lane t through {epoch,value} granules;
 //  * wave 0 = SOLVER.  The only work between node i-1's new mean and node i's
 //    is one d x 2r matvec with the fp64 base inverse B_i (rows in registers),
-//    one 20-value cross-lane reduction and 2x2 algebra:
+//    one 40-value cross-lane reduction (24 sums that involve mu_{i-1} and the 16
+//    that do not, formed from the lane's own registers) and 2x2 algebra:
 //       K_i  = B_i - L_{i-1} W_{i-1}^T + G_{i-1} X_{i-1}^T   (applied lazily)
 //       W_i  = K_i J_{i-1}^T ,  M_i = R + J_{i-1} W_i ,  L_i = W_i M_i^-1
 //       mu_i = u_i + W_i M_i^-1 (y_{i,i-1} - J_{i-1} u_i) ,  u_i = K_i g_i
@@ -26,12 +27,11 @@
 //           P_{i-1}^-1 = B_i - L_{i-1} W_{i-1}^T, damped and stored (hw 0-5);
 //       HE  h_obs GEMV of node i+2 over the slice's (U,V): register-resident
 //           (node j -> helper lane j % 448, slot j / 448), overflow in LDS;
-//       HF1 AR(1) terms + natural parameter g_{i+1} (hw 0-2);
-//       HF2 v_{i+1} = K_i g_{i+1}, yv_{i+1} = K_i J_{i+2}^T (hw 3-6);
-//       HX  the 20 dot products of the step that do not involve mu_{i-1} (hw 3);
+//       HF1 AR(1) terms + natural parameter g_{i+1} and node i+2's (U, V) for
+//           the solver's v = K_i g_{i+1}, yv = K_i J_{i+2}^T (hw 0-2);
 //       LOADER (hw 6): LDS-DMA (global_load_lds) rings, 3 steps ahead, for Y
-//           rows, old covariances, old means and the hand-off granules, so no
-//           wave holds prefetch registers.
+//           rows, old covariances and old means, so no wave holds prefetch
+//           registers; hw 5 reads the hand-off granules one step ahead.
 //  * one workgroup barrier per step; intra-step hand-offs through LDS
 //    counters;
 //  * the slice's base inverse P_0^-1 is formed in the prologue (fp64 sums over
@@ -137,16 +137,15 @@ struct Lay {
     static constexpr int oMu64 = al16(oRec + 8 * 2 * D * 8);       // [par][k] new mean (fp64)
     static constexpr int oMu32 = al16(oMu64 + 8 * 2 * D);          // [par][k] new mean (fp32)
     static constexpr int oG = al16(oMu32 + 4 * 2 * D);             // [node&1][k] g of node
-    static constexpr int oJn = al16(oG + 8 * 2 * D);               // [node&1][q][k] J rows of node i+2 (old)
+    static constexpr int oJn = al16(oG + 8 * 2 * D);               // [node&1][c] (U, V) of node i+2 (old, fp64)
     static constexpr int oV = al16(oJn + 8 * 4 * D);               // [node&1][k]{v, yv0, yv1, vA}
-    static constexpr int oDots = al16(oV + 8 * 2 * D * 4);         // HX results
-    static constexpr int oRed = al16(oDots + 8 * 32);              // solver reduction gather
+    static constexpr int oRed = al16(oV + 8 * 2 * D * 4);          // solver reduction gather (40 sums)
     static constexpr int oGP = al16(oRed + 8 * 64);                // [node&1][wave][k] GEMV partials
     static constexpr int oYst = al16(oGP + 4 * 2 * 7 * D);         // [node&3]{y(m,m-1), y(m,m-2)} raw
     static constexpr int oMuL = al16(oYst + 4 * 4 * 4);            // [wave][64] mu_{m,t-1}, zero padded
     static constexpr int oPd = al16(oMuL + 4 * 3 * 64);            // [par][k] naive diag(P)
     static constexpr int oPc = al16(oPd + 8 * 2 * D);              // [k] diag of Pconst(t) (naive)
-    static constexpr int oFlag = al16(oPc + 8 * D);                // kcnt, ddone, gcnt
+    static constexpr int oFlag = al16(oPc + 8 * D);                // kcnt, (unused), gcnt, (unused)
     static constexpr int oCr = al16(oFlag + 16);                   // [node&3] old covariances, DMA
     static constexpr int oXr = al16(oCr + 4 * 4 * cs);             // [node&7] old means slice t, DMA
     static constexpr int oRr = al16(oXr + 8 * 256);                // [node&3] old means slice t+1, DMA
@@ -201,7 +200,6 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     double* g64 = (double*)(smem + LY::oG);
     double* jn64 = (double*)(smem + LY::oJn);
     double* vbuf = (double*)(smem + LY::oV);          // prologue pivot scratch
-    double* dots = (double*)(smem + LY::oDots);
     double* red = (double*)(smem + LY::oRed);
     float* gp = (float*)(smem + LY::oGP);
     float* yst = (float*)(smem + LY::oYst);
@@ -210,7 +208,6 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     double* pcdl = (double*)(smem + LY::oPc);
     uint32_t* flags = (uint32_t*)(smem + LY::oFlag);
     uint32_t* kcnt = flags;
-    uint32_t* ddone = flags + 1;
     uint32_t* gcnt = flags + 2;
     float2* yring = (float2*)(smem + LY::oYr);
     float* cring = (float*)(smem + LY::oCr);
@@ -597,12 +594,26 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         const float* mr = rring + (m & 3) * 64;   // finite beyond D (padded coefficients are 0)
         const double* aq = arQ + kc * MCP + p * MC;
         const double* ap = arP + kc * MCP + p * MC;
+        // every LDS read first (one round trip), then the arithmetic
+        double av[MC], bv[MC];
+        float lv[MC], rv[MC], gv[7];
+#pragma unroll
+        for (int mm = 0; mm < MC; ++mm) {
+            av[mm] = aq[mm];
+            bv[mm] = ap[mm];
+            lv[mm] = ml[p * MC + mm];
+            rv[mm] = mr[p * MC + mm];
+        }
+#pragma unroll
+        for (int w = 0; w < 7; ++w) gv[w] = gp[((m & 1) * 7 + w) * D + kc];
+        const float mv2 = jcol_load<R>(mu32 + ((m - 2) & 1) * D, kc);
+        const float ys0 = yst[(m & 3) * 4 + 2], ys1 = yst[(m & 3) * 4 + 3];
+        __builtin_amdgcn_sched_barrier(0);
         double accL = 0.0, accR = 0.0;
 #pragma unroll
         for (int mm = 0; mm < MC; ++mm) {
-            const int c = p * MC + mm;
-            accL = fma(aq[mm], (double)ml[c], accL);
-            accR = fma(ap[mm], (double)mr[c], accR);
+            accL = fma(av[mm], (double)lv[mm], accL);
+            accR = fma(bv[mm], (double)rv[mm], accR);
         }
         double acc = accL + ((tg < Tt - 1) ? accR : 0.0);
         acc = dpp_add_xor1(acc);
@@ -610,27 +621,26 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         // lane (k, 0) assembles g_k = GEMV partials + AR + node m-2's term
         double g = 0.0;
 #pragma unroll
-        for (int w = 0; w < 7; ++w) g += (double)gp[((m & 1) * 7 + w) * D + kc];
+        for (int w = 0; w < 7; ++w) g += (double)gv[w];
         g += acc;
         if (m >= 2) {   // node m-2 was excluded from the GEMV; its new mean is known now
-            const float* mup = mu32 + ((m - 2) & 1) * D;
             double j0, j1;
-            jcol<R>(mup, true, kc, j0, j1);
-            const double y0 = (double)yst[(m & 3) * 4 + 2], y1 = (double)yst[(m & 3) * 4 + 3];
+            jcol_sel<R>(mv2, true, kc, j0, j1);
+            const double y0 = (double)ys0, y1 = (double)ys1;
             const double z0 = r00 * y0 + r01 * y1, z1 = r10 * y0 + r11 * y1;
             g = fma(j0, z0, fma(j1, z1, g));
         }
         if (k < D && p == 0) g64[(m & 1) * D + k] = g;
     };
-    // J rows of `node` (old) -> jn64 slot node & 1 (lanes < D of the calling wave).
-    // Double-buffered: hw 0 fills node i+2 during step i while the solver may
-    // still be reading node i+1's (its prologue prep of step 0 overlaps step 0)
+    // (U, V) of `node` (old, fp64) -> jn64 slot node & 1 (lanes < 2r of the calling
+    // wave): the only non-constant entries of its J rows J0 = [1, 0, V, 0],
+    // J1 = [0, 1, 0, U].  Double-buffered: hw 0 fills node i+2 during step i while
+    // the solver may still be reading node i+1's (its prologue prep of step 0
+    // overlaps step 0)
     auto jn_fill = [&](int node) {
-        if (lane < D) {
-            double j0, j1;
-            jcol<R>(xring + (node & 7) * 64, node < n, lane, j0, j1);
-            jn64[(node & 1) * 2 * D + lane] = j0;
-            jn64[(node & 1) * 2 * D + D + lane] = j1;
+        if (lane < M2) {
+            const float* xm = xring + (node & 7) * 64;
+            jn64[(node & 1) * 2 * D + lane] = (node < n) ? (double)xm[2 + lane] : 0.0;
         }
     };
 
@@ -693,29 +703,38 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
 #pragma unroll
         for (int c = 0; c < D; ++c) brow[c] = kl ? Kbuf[(size_t)k * KS + c] : 0.0;
         // v = B g, yv = B Jn^T (Jn: J rows of node i+1, old) and this lane's Jn
-        // entries, for the coming step; B = brow, g and Jn from HF1 / jn_fill.
-        // Runs at the end of the previous step, after the solver's own work.
+        // entries, for the coming step; B = brow, g and node i+1's (U, V) from
+        // HF1 / jn_fill.  J0 = [1, 0, V, 0], J1 = [0, 1, 0, U]: yv needs 2r
+        // products, not 2d.  Runs at the end of the previous step, after the
+        // solver's own work.
         double v = 0, yv0 = 0, yv1 = 0, vA = 0, nq0 = 0, nq1 = 0;
         auto prep = [&](int node) {
-            const double* jn = jn64 + ((node + 1) & 1) * 2 * D;   // J rows of node + 1
+            const double* jx = jn64 + ((node + 1) & 1) * 2 * D;   // (U, V) of node + 1
             if (!kl) return;
             const double* gg = g64 + (node & 1) * D;
-            double s0 = 0, s1 = 0, s2 = 0, t0 = 0, t1 = 0, t2 = 0;
+            const bool ex1 = node + 1 < n;                          // J of a missing node is 0
+            double s0 = 0, t0 = 0, s1 = ex1 ? brow[0] : 0.0, t1 = 0, s2 = ex1 ? brow[1] : 0.0, t2 = 0;
 #pragma unroll
             for (int c = 0; c < D; c += 2) {
                 s0 = fma(brow[c], gg[c], s0);
-                s1 = fma(brow[c], jn[c], s1);
-                s2 = fma(brow[c], jn[D + c], s2);
                 t0 = fma(brow[c + 1], gg[c + 1], t0);
-                t1 = fma(brow[c + 1], jn[c + 1], t1);
-                t2 = fma(brow[c + 1], jn[D + c + 1], t2);
+            }
+#pragma unroll
+            for (int c = 0; c < R; c += 2) {
+                s1 = fma(brow[2 + c], jx[R + c], s1);       // J0: V at columns 2 .. 2+R
+                s2 = fma(brow[2 + R + c], jx[c], s2);       // J1: U at columns 2+R .. D
+                if (c + 1 < R) {
+                    t1 = fma(brow[3 + c], jx[R + c + 1], t1);
+                    t2 = fma(brow[3 + R + c], jx[c + 1], t2);
+                }
             }
             v = s0 + t0;
             yv0 = s1 + t1;
             yv1 = s2 + t2;
             vA = brow[0] * gg[0] + brow[1] * gg[1];
-            nq0 = jn[k];
-            nq1 = jn[D + k];
+            const double xj = jx[(k >= 2 && k < 2 + R) ? k - 2 + R : ((k >= 2 + R && k < D) ? k - 2 - R : 0)];
+            nq0 = (k == 0) ? (ex1 ? 1.0 : 0.0) : ((k >= 2 && k < 2 + R) ? xj : 0.0);
+            nq1 = (k == 1) ? (ex1 ? 1.0 : 0.0) : ((k >= 2 + R && k < D) ? xj : 0.0);
         };
         prep(0);
         double Wp0 = 0, Wp1 = 0, Xp0 = 0, Xp1 = 0, Lp0 = 0, Lp1 = 0, Gp0 = 0, Gp1 = 0;
@@ -748,8 +767,12 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 kj1 = s1a + s1b;
             }
             STAMP3(1);
-            // critical reduction: a1(4) a2(4) c(4) e(2) jy(4) eA(2) ny(4)
-            constexpr int NV = 24;
+            // one reduction per step: a1(4) a2(4) c(4) e(2) jy(4) eA(2) ny(4), and the
+            // dots that do not involve mu_{i-1}: b1(2) b2(2) f1(4) f2(4) b1A(2) b2A(2)
+            // (W, X of the previous step, g_i and node i+1's J entries are this
+            // lane's own registers; until round 3 a helper wave formed them, "HX",
+            // and the solver waited for it: profiles/r03_v3_ab_hx_in_solver.txt)
+            constexpr int NV = 40;
             double pr[NV];
             pr[0] = Wp0 * J0; pr[1] = Wp0 * J1; pr[2] = Wp1 * J0; pr[3] = Wp1 * J1;       // a1[p][q]
             pr[4] = Xp0 * J0; pr[5] = Xp0 * J1; pr[6] = Xp1 * J0; pr[7] = Xp1 * J1;       // a2[p][q]
@@ -758,6 +781,13 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             pr[14] = J0 * yv0; pr[15] = J0 * yv1; pr[16] = J1 * yv0; pr[17] = J1 * yv1;   // jy[q][p]
             pr[18] = J0 * vA; pr[19] = J1 * vA;                                           // eA[q]
             pr[20] = nq0 * yv0; pr[21] = nq0 * yv1; pr[22] = nq1 * yv0; pr[23] = nq1 * yv1;   // ny[q][p]
+            {
+                const double gA = (k < 2) ? g : 0.0;
+                pr[24] = Wp0 * g; pr[25] = Wp1 * g; pr[26] = Xp0 * g; pr[27] = Xp1 * g;           // b1, b2
+                pr[28] = Wp0 * nq0; pr[29] = Wp0 * nq1; pr[30] = Wp1 * nq0; pr[31] = Wp1 * nq1;   // f1[p][q]
+                pr[32] = Xp0 * nq0; pr[33] = Xp0 * nq1; pr[34] = Xp1 * nq0; pr[35] = Xp1 * nq1;   // f2[p][q]
+                pr[36] = Wp0 * gA; pr[37] = Wp1 * gA; pr[38] = Xp0 * gA; pr[39] = Xp1 * gA;       // b1A, b2A
+            }
             {
                 int idx;
                 const double sv = wave_reduce_scatter<NV>(pr, lane, idx);
@@ -775,13 +805,11 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             const V2 eA = {o[18], o[19]};
             const Mat2 ny = m2(o[20], o[21], o[22], o[23]);
             STAMP3(2);
-            // off-critical dots from helper wave hw 5
-            lds_wait_ge(ddone, (uint32_t)(i + 1), a.status, dead);
             STAMP3(3);
-            const V2 b1 = {dots[0], dots[1]}, b2 = {dots[2], dots[3]};
-            const Mat2 f1 = m2(dots[4], dots[5], dots[6], dots[7]);
-            const Mat2 f2 = m2(dots[8], dots[9], dots[10], dots[11]);
-            const V2 b1A = {dots[12], dots[13]}, b2A = {dots[14], dots[15]};
+            const V2 b1 = {o[24], o[25]}, b2 = {o[26], o[27]};
+            const Mat2 f1 = m2(o[28], o[29], o[30], o[31]);
+            const Mat2 f2 = m2(o[32], o[33], o[34], o[35]);
+            const V2 b1A = {o[36], o[37]}, b2A = {o[38], o[39]};
             // raw y_{i,i-1}
             double y0 = 0, y1 = 0;
             if (has_prev) { y0 = (double)yst[(i & 3) * 4 + 0]; y1 = (double)yst[(i & 3) * 4 + 1]; }
@@ -929,28 +957,6 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 pgr = (tl == 0) ? gran_load_system(gran_src(i + 2) + lane)
                                 : gran_load_agent(gran_src(i + 2) + lane);
 #endif
-            // HX (hw 5, off the solver's SIMD): dots that do not involve mu_{i-1}
-            if (hw == 5 && i < n) {
-                const int k = lane;
-                const int kc = (k < D) ? k : 0;
-                const double msk = (k < D) ? 1.0 : 0.0;
-                const double* rc = rec + (size_t)ppar * 8 * D + kc;
-                const double W0 = msk * rc[2 * D], W1 = msk * rc[3 * D], X0 = msk * rc[6 * D], X1 = msk * rc[7 * D];
-                const double g = g64[par * D + kc];
-                double n0, n1;
-                jcol<R>(xring + ((i + 1) & 7) * 64, i + 1 < n, kc, n0, n1);
-                const double gA = (k < 2) ? g : 0.0;
-                double pr[16];
-                pr[0] = W0 * g; pr[1] = W1 * g; pr[2] = X0 * g; pr[3] = X1 * g;           // b1, b2
-                pr[4] = W0 * n0; pr[5] = W0 * n1; pr[6] = W1 * n0; pr[7] = W1 * n1;       // f1[p][q]
-                pr[8] = X0 * n0; pr[9] = X0 * n1; pr[10] = X1 * n0; pr[11] = X1 * n1;     // f2[p][q]
-                pr[12] = W0 * gA; pr[13] = W1 * gA; pr[14] = X0 * gA; pr[15] = X1 * gA;   // b1A, b2A
-                int idx;
-                const double sv = wave_reduce_scatter<16>(pr, lane, idx);
-                if (idx < 16) dots[idx] = sv;
-                if (lane == 0) lds_signal_set(ddone, (uint32_t)(i + 1));
-                STAMP3(1);
-            }
             // HB (hw 0..5): K_i = B_i - L W^T + G X^T, fused covariance of node i-1
             if (hw <= 5) {
                 const double* rp = rec + (size_t)ppar * 8 * D;   // [field][k]

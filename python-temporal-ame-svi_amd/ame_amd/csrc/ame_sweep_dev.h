@@ -98,6 +98,22 @@ __device__ __forceinline__ void tri_decode3(int e, int& k, int& m) {
     m = e - k * (k + 1) / 2;
 }
 
+// jcol in two halves, so the LDS read can be issued ahead of its use:
+// jcol_load reads the one mean entry row k needs, jcol_sel forms J's entries.
+template <int R>
+__device__ __forceinline__ float jcol_load(const float* mu, int k) {
+    constexpr int D = 2 + 2 * R;
+    const int src = (k < 2 + R) ? (k + R) : (k - R);
+    return mu[(k >= 2 && k < D) ? src : 0];
+}
+template <int R>
+__device__ __forceinline__ void jcol_sel(float mv, bool exists, int k, double& j0, double& j1) {
+    constexpr int D = 2 + 2 * R;
+    const double v = (double)mv;
+    j0 = !exists ? 0.0 : (k == 0) ? 1.0 : (k >= 2 && k < 2 + R) ? v : 0.0;
+    j1 = !exists ? 0.0 : (k == 1) ? 1.0 : (k >= 2 + R && k < D) ? v : 0.0;
+}
+
 // J entries of a node for state index k, from its (fp32) mean in LDS:
 // J = [[1, 0, V, 0], [0, 1, 0, U]]; zero when the node does not exist.
 template <int R>
