@@ -47,6 +47,20 @@
 
 using namespace ame;
 
+namespace {
+// 2x2 inverse with the reciprocal of the determinant from v_rcp_f64 plus two
+// Newton steps (instead of the IEEE division sequence): full fp64 accuracy for
+// the well-scaled determinants here, a shorter dependent chain
+__device__ __forceinline__ Mat2 inv2s_fast(Mat2 m) {
+    const double det = m.a * m.d - m.b * m.c;
+    double r = __builtin_amdgcn_rcp(det);
+    r = fma(r, fma(-det, r, 1.0), r);
+    r = fma(r, fma(-det, r, 1.0), r);
+    const double o = 0.5 * (-m.b * r - m.c * r);
+    return {m.d * r, o, o, m.a * r};
+}
+}  // namespace
+
 #ifdef AME_STAMPS
 // Diagnostic build only (cdna_hip_programming.md §7, in-kernel stamps): the
 // middle lane records s_memtime at marked points of steps [S3_I0, S3_I0+16) for
@@ -133,8 +147,9 @@ struct Lay {
     static constexpr int KS = D + 1;                               // base inverse row stride (odd: no bank conflicts)
     static constexpr int KSZ = D * KS;
     static constexpr int oAR = al16(oK + 8 * 2 * KSZ);             // Qinv Phi, Phi^T Qinv (fp64) [D][MCP]
-    static constexpr int oRec = al16(oAR + 8 * 2 * D * MCP);       // [par]{L0 L1 W0 W1 G0 G1 X0 X1}[k]
-    static constexpr int oMu64 = al16(oRec + 8 * 2 * D * 8);       // [par][k] new mean (fp64)
+    static constexpr int RS = 10;                                  // rec row stride (doubles)
+    static constexpr int oRec = al16(oAR + 8 * 2 * D * MCP);       // [par][k][RS]: L0 L1 W0 W1 G0 G1 X0 X1
+    static constexpr int oMu64 = al16(oRec + 8 * 2 * D * RS);      // [par][k] new mean (fp64)
     static constexpr int oMu32 = al16(oMu64 + 8 * 2 * D);          // [par][k] new mean (fp32)
     static constexpr int oG = al16(oMu32 + 4 * 2 * D);             // [node&1][k] g of node
     static constexpr int oJn = al16(oG + 8 * 2 * D);               // [node&1][c] (U, V) of node i+2 (old, fp64)
@@ -465,7 +480,8 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     }
     for (int e = tid; e < 3 * 64; e += kNT) muL[e] = 0.f;
     if (tid < D) pcdl[tid] = pconst_entry(a.consts, D, tid, tid, tg, Tt);
-    for (int e = tid; e < 2 * D * 8; e += kNT) rec[e] = 0.0;
+    constexpr int RS = LY::RS;
+    for (int e = tid; e < 2 * D * RS; e += kNT) rec[e] = 0.0;
     for (int e = tid; e < 2 * D; e += kNT) {
         mu64[e] = 0.0;
         mu32[e] = 0.f;
@@ -817,14 +833,14 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             // ---- 2x2 algebra ----
             const Mat2 JW = add(sub(cc, quad(a1, Mip, a1)), quad(a2, Sip, a2));
             const Mat2 Mm = add(Rm, sym(JW));
-            const Mat2 Mi = has_prev ? inv2s(Mm) : m2(0, 0, 0, 0);
+            const Mat2 Mi = has_prev ? inv2s_fast(Mm) : m2(0, 0, 0, 0);
             const V2 t1 = mtv(a1, mv(Mip, b1)), t2 = mtv(a2, mv(Sip, b2));
             const V2 Ju = {e.x - t1.x + t2.x, e.y - t1.y + t2.y};
             const V2 cvec = mv(Mi, V2{y0 - Ju.x, y1 - Ju.y});
             const Mat2 wn = add(sub(jy, quad(a1, Mip, f1)), quad(a2, Sip, f2));
             const Mat2 JnK = add(sub(ny, quad(f1, Mip, f1)), quad(f2, Sip, f2));
             const Mat2 JnX = sub(JnK, quad(wn, Mi, wn));
-            const Mat2 Si = inv2s(sub(Rm, sym(JnX)));
+            const Mat2 Si = inv2s_fast(sub(Rm, sym(JnX)));
             // ---- lane-local assembly ----
             const double W0 = kj0 - (Lp0 * a1.a + Lp1 * a1.c) + (Gp0 * a2.a + Gp1 * a2.c);
             const double W1 = kj1 - (Lp0 * a1.b + Lp1 * a1.d) + (Gp0 * a2.b + Gp1 * a2.d);
@@ -839,10 +855,10 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 const V2 s1 = mtv(a1, mv(Mip, b1A)), s2 = mtv(a2, mv(Sip, b2A));
                 const V2 JuA = {eA.x - s1.x + s2.x, eA.y - s1.y + s2.y};
                 // K_i[:, 0:2] (row k) and W_i rows 0, 1 (uniform)
-                const double* rq = rec + (size_t)ppar * 8 * D;   // [field][k]
-                const double KE0 = brow[0] - (Lp0 * rq[2 * D] + Lp1 * rq[3 * D]) + (Gp0 * rq[6 * D] + Gp1 * rq[7 * D]);
-                const double KE1 = brow[1] - (Lp0 * rq[2 * D + 1] + Lp1 * rq[3 * D + 1]) +
-                                   (Gp0 * rq[6 * D + 1] + Gp1 * rq[7 * D + 1]);
+                const double* rq = rec + (size_t)ppar * D * RS;   // [k][field]
+                const double KE0 = brow[0] - (Lp0 * rq[2] + Lp1 * rq[3]) + (Gp0 * rq[6] + Gp1 * rq[7]);
+                const double KE1 = brow[1] - (Lp0 * rq[RS + 2] + Lp1 * rq[RS + 3]) +
+                                   (Gp0 * rq[RS + 6] + Gp1 * rq[RS + 7]);
                 const double WE00 = __shfl(W0, 0), WE01 = __shfl(W1, 0);   // W row 0
                 const double WE10 = __shfl(W0, 1), WE11 = __shfl(W1, 1);   // W row 1
                 const double wz0 = WE00 * zp0 + WE10 * zp1, wz1 = WE01 * zp0 + WE11 * zp1;
@@ -878,9 +894,9 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                     gran_store_system(a.halo_out + (size_t)i * D + k, gr);
                 mu32[par * D + k] = nw;
                 mu64[par * D + k] = (double)nw;
-                double* rc = rec + (size_t)par * 8 * D + k;   // [field][k]
-                rc[0] = Ln0; rc[D] = Ln1; rc[2 * D] = W0; rc[3 * D] = W1;
-                rc[4 * D] = Gn0; rc[5 * D] = Gn1; rc[6 * D] = Xn0; rc[7 * D] = Xn1;
+                double* rc = rec + ((size_t)par * D + k) * RS;   // [k][field]
+                rc[0] = Ln0; rc[1] = Ln1; rc[2] = W0; rc[3] = W1;
+                rc[4] = Gn0; rc[5] = Gn1; rc[6] = Xn0; rc[7] = Xn1;
                 if (is_naive) {
                     const double p = r00, s = r11;
                     double pd;
@@ -959,7 +975,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
 #endif
             // HB (hw 0..5): K_i = B_i - L W^T + G X^T, fused covariance of node i-1
             if (hw <= 5) {
-                const double* rp = rec + (size_t)ppar * 8 * D;   // [field][k]
+                const double* rp = rec + (size_t)ppar * D * RS;   // [k][field]
                 const double* pdp = pdl + (size_t)ppar * D;
                 const float* co = cring + (size_t)((i + 3) & 3) * LY::cs;   // node i-1
                 float* cv = cst + (size_t)(i & 1) * LY::cs;                  // node i-1, staged
@@ -967,12 +983,12 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 for (int q = 0; q < LTQ; ++q) {
                     const bool ok = lk[q] >= 0;
                     const int k = ok ? lk[q] : 0, m = ok ? lm[q] : 0;
-                    const double* rk = rp + k;
-                    const double* rm = rp + m;
+                    const double* rk = rp + k * RS;
+                    const double* rm = rp + m * RS;
                     const double bkm = Bi[k * KS + m];
                     const float ckm = co[k * D + m], cmk = co[m * D + k];
-                    const double c = bkm - (rk[0] * rm[2 * D] + rk[D] * rm[3 * D]);
-                    const double kn = c + (rk[4 * D] * rm[6 * D] + rk[5 * D] * rm[7 * D]);
+                    const double c = bkm - (rk[0] * rm[2] + rk[1] * rm[3]);
+                    const double kn = c + (rk[4] * rm[6] + rk[5] * rm[7]);
                     float c32;
                     if (is_naive) {
                         c32 = (k == m) ? 1.0f / ((float)pdp[k] + 1e-8f) : 0.f;
