@@ -876,17 +876,12 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             const double Xn1 = kn1 - (Ln0 * wn.b + Ln1 * wn.d);
             const double Gn0 = Xn0 * Si.a + Xn1 * Si.c, Gn1 = Xn0 * Si.b + Xn1 * Si.d;
             STAMP3(4);
-            // naive: diag(P_i) from running sums of squares (own old value removed)
-            double sq_other = 0.0;
-            if (is_naive) {
-                const int src = (k >= 2 && k < 2 + R) ? k + R : ((k >= 2 + R && k < D) ? k - R : k);
-                sq_other = __shfl(ssq_l, src);
-            }
             // ---- publish ----
+            float mold = 0.f, nw = 0.f;
             if (kl) {
                 const float* xold = xring + (i & 7) * 64;
-                const float mold = xold[k];
-                const float nw = __fadd_rn(__fmul_rn(lr, (float)mus), __fmul_rn(om, mold));
+                mold = xold[k];
+                nw = __fadd_rn(__fmul_rn(lr, (float)mus), __fmul_rn(om, mold));
                 xn[(size_t)i * D + k] = nw;
                 const uint64_t gr = ((uint64_t)a.epoch << 32) | (uint64_t)__float_as_uint(nw);
                 gran_store_agent(a.hand + ((size_t)tl * n + i) * D + k, gr);
@@ -897,7 +892,15 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 double* rc = rec + ((size_t)par * D + k) * RS;   // [k][field]
                 rc[0] = Ln0; rc[1] = Ln1; rc[2] = W0; rc[3] = W1;
                 rc[4] = Gn0; rc[5] = Gn1; rc[6] = Xn0; rc[7] = Xn1;
-                if (is_naive) {
+            }
+            // naive: diag(P_i) from running sums of squares (own old value removed),
+            // for node i's covariance (HB, next step); after the mean is published,
+            // so its cross-lane read is off the mean's path
+            if (is_naive) {
+                const int src = (k >= 2 && k < 2 + R) ? k + R : ((k >= 2 + R && k < D) ? k - R : k);
+                const double sq_other = __shfl(ssq_l, src);
+                if (kl) {
+                    const float* xold = xring + (i & 7) * 64;
                     const double p = r00, s = r11;
                     double pd;
                     if (k == 0) pd = p * (double)(n - 1);
