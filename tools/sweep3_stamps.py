@@ -26,12 +26,12 @@ def _unsplit_sources():
     return UNSPLIT_SOURCES
 
 NAMES = {   # stamp slot names per wave (the kernel stamps every wave; see ame_sweep3.hip STAMP3)
-    0: ["start", "J+kj", "reduce", "ddone", "2x2+assembly", "publish", "kcnt", "brow", "gcnt", "prep(v,yv)"],
+    0: ["start", "J+kj", "reduce", "(was: HX wait)", "2x2+assembly", "publish", "kcnt", "brow", "gcnt", "prep(v,yv)"],
 }
 for _w in range(1, 8):
     _hw = _w - 1
     NAMES[_w] = ["start",
-                 "HX" if _hw == 5 else ("pring" if _hw <= 2 else "-"),
+                 "pring" if _hw <= 2 else "-",
                  "poll" if _hw <= 2 else "-",
                  "hf1" if _hw <= 2 else "-",
                  "HB" if _hw <= 5 else "(no HB)",
