@@ -1,8 +1,8 @@
 """Does the ELBO side (covariance-terms + ELBO kernels, run beside the pipelined
-sweeps) slow the sweep down?  Config 3, one GPU:
+sweeps) slow the sweep down?  Config 3 by default, one GPU:
 
     python tools/interference.py --build TAG DEF1,DEF2   # here: variant library _build/libame_amd_var{TAG}.so
-    python tools/interference.py [TAG ...]               # GPU box: per library, fit vs sweeps-only
+    python tools/interference.py [--shape n,T,r] [TAG ...]   # GPU box: per library, fit vs sweeps-only
 
 (A) ms per fit() iteration (the bench's loop); (B) ms per sweep when the same
 pipelined, two-deep sweep queue runs with no ELBO side at all.  Diagnostic
@@ -43,12 +43,12 @@ def build(tag, defs):
     print("built", so)
 
 
-def measure(K=20):
+def measure(K=20, shape=(1024, 128, 16)):
     sys.path.insert(0, PKG)
     import torch
     from ame_amd import TemporalAMEModel, TemporalAMEStructuredMFVI
     dev = torch.device("cuda", 0)
-    m = TemporalAMEModel(1024, 128, 16, seed=42)
+    m = TemporalAMEModel(*shape, seed=42)
     m.generate_data_fast(device=dev)
     vi = TemporalAMEStructuredMFVI(m, factorization="good", learning_rate=0.01, device=dev)
     vi.fit(max_iter=3, tolerance=0.0, verbose=False)
@@ -74,7 +74,8 @@ def measure(K=20):
         torch.cuda.synchronize()
         res[label] = (time.perf_counter() - t0) * 1e3 / K
     eng._check_status()
-    return {"fit_ms_per_iter": fit_ms, **{k + "_ms": v for k, v in res.items()},
+    return {"shape": list(shape), "sweep_kind": int(eng.sweep_kind), "pipelined": bool(eng.pipelined),
+            "fit_ms_per_iter": fit_ms, **{k + "_ms": v for k, v in res.items()},
             "lib": os.environ.get("AME_LIB_PATH", "default")}
 
 
@@ -83,14 +84,22 @@ if __name__ == "__main__":
         k = sys.argv.index("--build")
         build(sys.argv[k + 1], sys.argv[k + 2].split(",") if len(sys.argv) > k + 2 else [])
     elif "--child" in sys.argv:
-        print(json.dumps(measure()))
+        shape = tuple(int(x) for x in sys.argv[sys.argv.index("--child") + 1].split(","))
+        K = 20 if shape[0] <= 1024 else 8
+        print(json.dumps(measure(K, shape)))
     else:
-        for tag in ["default"] + [a for a in sys.argv[1:]]:
+        args = sys.argv[1:]
+        shape = "1024,128,16"
+        if "--shape" in args:
+            k = args.index("--shape")
+            shape = args[k + 1]
+            del args[k:k + 2]
+        for tag in ["default"] + args:
             env = dict(os.environ)
             if tag != "default":
                 env["AME_LIB_PATH"] = os.path.join(BDIR, f"libame_amd_var{tag}.so")
             for rep in range(2):
-                r = subprocess.run([sys.executable, "-u", __file__, "--child"], env=env, capture_output=True,
+                r = subprocess.run([sys.executable, "-u", __file__, "--child", shape], env=env, capture_output=True,
                                    text=True, timeout=300)
                 if r.returncode != 0:
                     print(tag, "failed", r.stderr[-2000:])
