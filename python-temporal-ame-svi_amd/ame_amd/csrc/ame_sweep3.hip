@@ -189,7 +189,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     // XCD-aware lane order: consecutive time slices share an XCD (speed only)
     const int tl = (TL % 8 == 0) ? ((b & 7) * (TL >> 3) + (b >> 3)) : b;
     const int tg = dm.t_begin + tl;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int hl = tid - 64, hw = wave - 1;   // helper lane / helper wave (valid for wave >= 1)
     const int hj = (hl + kNH - kGOFF) % kNH;    // first node of helper lane hl (slot 0)
     const bool is_naive = dm.variant == AME_NAIVE, is_bad = dm.variant == AME_BAD;
@@ -970,11 +970,19 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             // Loaded with 8-byte atomic loads, not LDS-DMA: a 16-byte DMA that
             // races the producer's store may see a granule half-written (new epoch,
             // old value), which the epoch check cannot tell apart.
-            uint64_t pgr = 0;
+            // (set and consumed only inside hw 5's branches, so the compiler's wait
+            // on this register's previous load stays out of the other waves' path --
+            // a vmcnt(0) there would also drain the loader's LDS-DMA and hw 4's
+            // covariance stores at every step start)
+            uint64_t pgr;
 #ifndef AME_S3_OLDP
-            if (hw == 5 && i + 2 < n && tg > 0 && lane < D)
-                pgr = (tl == 0) ? gran_load_system(gran_src(i + 2) + lane)
-                                : gran_load_agent(gran_src(i + 2) + lane);
+            if (hw == 5) {
+                if (i + 2 < n && tg > 0 && lane < D)
+                    pgr = (tl == 0) ? gran_load_system(gran_src(i + 2) + lane)
+                                    : gran_load_agent(gran_src(i + 2) + lane);
+                else
+                    pgr = 0;
+            }
 #endif
             // HB (hw 0..5): K_i = B_i - L W^T + G X^T, fused covariance of node i-1
             if (hw <= 5) {
