@@ -160,7 +160,8 @@ struct Lay {
     static constexpr int oMuL = al16(oYst + 4 * 4 * 4);            // [wave][64] mu_{m,t-1}, zero padded
     static constexpr int oPd = al16(oMuL + 4 * 3 * 64);            // [par][k] naive diag(P)
     static constexpr int oPc = al16(oPd + 8 * 2 * D);              // [k] diag of Pconst(t) (naive)
-    static constexpr int oFlag = al16(oPc + 8 * D);                // kcnt, (unused), gcnt, (unused)
+    static constexpr int oSq = al16(oPc + 8 * D);                  // [k] naive running column sums of squares
+    static constexpr int oFlag = al16(oSq + 8 * D);                // kcnt, (unused), gcnt, (unused)
     static constexpr int oCr = al16(oFlag + 16);                   // [node&3] old covariances, DMA
     static constexpr int oXr = al16(oCr + 4 * 4 * cs);             // [node&7] old means slice t, DMA
     static constexpr int oRr = al16(oXr + 8 * 256);                // [node&3] old means slice t+1, DMA
@@ -221,6 +222,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     float* muL = (float*)(smem + LY::oMuL);
     double* pdl = (double*)(smem + LY::oPd);
     double* pcdl = (double*)(smem + LY::oPc);
+    double* ssq = (double*)(smem + LY::oSq);
     uint32_t* flags = (uint32_t*)(smem + LY::oFlag);
     uint32_t* kcnt = flags;
     uint32_t* gcnt = flags + 2;
@@ -378,7 +380,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     }
     // P_0 = Pconst + sum_{j>=1} F_j(old), F_j = J_j^T R^-1 J_j (fp64), and its
     // inverse -> Kbuf[0] by the in-place symmetric sweep operator; naive variant:
-    // column sums of squares of (U, V) over all nodes -> red[]
+    // column sums of squares of (U, V) over all nodes -> ssq[2 + c]
     {
         constexpr int EQ = (NLT + kNT - 1) / kNT;
         float* st = (float*)yring;   // staging: CH nodes x 2r (the rings are not live yet)
@@ -431,7 +433,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         }
         if (tid < M2) {   // node 0 joins the sums of squares
             const double v = (double)xo[2 + tid];
-            red[tid] = fma(v, v, sq);
+            ssq[2 + tid] = fma(v, v, sq);
         }
 #pragma unroll
         for (int u = 0; u < EQ; ++u) {
@@ -516,8 +518,6 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                                                     : make_float2(0.f, 0.f);
         }
     }
-    double ssq_l = 0.0;   // solver, naive: running sum of squares of column `lane`
-    if (tid < D && is_naive && tid >= 2) ssq_l = red[tid - 2];
     if (wave == 7) {   // rings read by steps 0..2 and the prologue
         for (int q = 0; q < 5; ++q) dma_x(q);
         for (int q = 0; q < 4; ++q) dma_r(q);
@@ -898,7 +898,6 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             // so its cross-lane read is off the mean's path
             if (is_naive) {
                 const int src = (k >= 2 && k < 2 + R) ? k + R : ((k >= 2 + R && k < D) ? k - R : k);
-                const double sq_other = __shfl(ssq_l, src);
                 if (kl) {
                     const float* xold = xring + (i & 7) * 64;
                     const double p = r00, s = r11;
@@ -907,11 +906,13 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                     else if (k == 1) pd = s * (double)(n - 1);
                     else {
                         const double oo = (k < 2 + R) ? (double)xold[k + R] : (double)xold[k - R];
-                        pd = ((k < 2 + R) ? p : s) * (sq_other - oo * oo);
+                        pd = ((k < 2 + R) ? p : s) * (ssq[src] - oo * oo);
                     }
                     pdl[par * D + k] = pd + pcdl[k];
                     const double mo = (double)mold, mn = (double)nw;
-                    if (k >= 2) ssq_l = ssq_l - mo * mo + mn * mn;
+                    // LDS, not a register: a loop-carried naive-only value spills
+                    // (256-VGPR cap) and its reload waits on the publish stores
+                    if (k >= 2) ssq[k] = ssq[k] - mo * mo + mn * mn;
                 }
             }
             Wp0 = W0; Wp1 = W1; Xp0 = Xn0; Xp1 = Xn1; Lp0 = Ln0; Lp1 = Ln1; Gp0 = Gn0; Gp1 = Gn1;
