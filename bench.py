@@ -62,15 +62,39 @@ def _host_info():
     return {"host_cpus": os.cpu_count(), "cpu_model": model}
 
 
-def cpu_baseline(model, vi, n, T, d, budget_s=24.0):
-    """Time the CPU restatements (fp32, the reference's dtype) on bounded
-    samples of the same iteration and extrapolate to one full iteration.
+def _committed_full_iteration(n, T, r):
+    """Full-iteration CPU measurements of the direct numpy restatement committed
+    by tools/cpu_baselines.py (profiles/r03_cpu_baselines.jsonl) for this shape."""
+    path = os.path.join(ROOT, "profiles", "r03_cpu_baselines.jsonl")
+    out = []
+    if os.path.exists(path):
+        for line in open(path):
+            try:
+                z = json.loads(line)
+            except ValueError:
+                continue
+            if (z.get("n"), z.get("T"), z.get("latent_dim")) == (n, T, r) and z.get("full_iteration"):
+                out.append({k: z.get(k) for k in ("kind", "threads", "s_per_iteration", "units_per_s",
+                                                  "cpu_model")})
+    return out or None
 
-    * main value: the vectorised numpy oracle (oracle/ame_oracle.py; BLAS
-      threads = the threads numpy uses on this host), SURVEY.md §8d(ii);
-    * ``loop_restatement``: oracle/ame_loop_oracle.py, the reference's cost
-      model (one small torch op sequence per ordered dyad / unordered pair,
-      structured_mf.py:130-148, :303-324), SURVEY.md §8d(i).
+
+def cpu_baseline(model, vi, n, T, d, budget_s=40.0):
+    """CPU baselines on this host, fp64 / fp32 restatements of the same iteration
+    (SURVEY.md §8d), timed after the GPU's timed region:
+
+    * main value: the vectorised numpy oracle in its statistics form
+      (oracle/ame_oracle.py sweep_stats + elbo_recon_fast, fp64, BLAS threads as
+      numpy uses them): ONE FULL ITERATION measured, not extrapolated, when the
+      sweep's estimate fits `budget_s` (config 3: it does); otherwise the sweep
+      is timed on a node prefix and extrapolated (said in `sample`);
+    * ``direct_restatement``: the per-step restatement (update_node: P_obs / h_obs
+      summed over all other nodes at every step, as the reference does) on a
+      node sample, extrapolated; plus its committed full-iteration figures
+      for this shape, if any (tools/cpu_baselines.py);
+    * ``loop_restatement``: oracle/ame_loop_oracle.py, the reference's cost model
+      (one small torch op sequence per ordered dyad / unordered pair,
+      structured_mf.py:130-148, :303-324), 1 core, on a sample, extrapolated.
     """
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ame_oracle as O
@@ -80,47 +104,49 @@ def cpu_baseline(model, vi, n, T, d, budget_s=24.0):
         threads = max([p.get("num_threads", 1) for p in threadpool_info()] + [1])
     except Exception:  # pragma: no cover
         threads = 1
+    r = (d - 2) // 2
     Y = model.Y.detach().cpu().numpy().astype(np.float32)
-    Xm = vi.X_mean.numpy().astype(np.float32).copy()
-    Xc = vi.X_cov.numpy().astype(np.float32).copy()
+    X32 = vi.X_mean.numpy().astype(np.float32).copy()
+    C32 = vi.X_cov.numpy().astype(np.float32).copy()
     params = {k: getattr(model, k).detach().cpu().numpy().astype(np.float32)
               for k in ("R", "R_inv", "Sigma", "Psi", "Phi", "Q")}
-    consts = O.prior_terms(params, T, np.float32)
-    # --- vectorised oracle: a block of nodes of the sweep ---
-    t0 = time.perf_counter()
-    O.update_node(Y, Xm, Xc, params, 0, "good", 0.01, consts)
-    per_node = time.perf_counter() - t0
-    k = int(max(1, min(n - 1, (0.6 * budget_s) / max(per_node, 1e-6))))
-    t0 = time.perf_counter()
-    for i in range(1, 1 + k):
-        O.update_node(Y, Xm, Xc, params, i, "good", 0.01, consts)
-    sweep_est = (time.perf_counter() - t0) / k * n
-    # loglik + MSE on a set of whole slices
-    t0 = time.perf_counter()
-    O.expected_loglik(Y, Xm, Xc, params, "good", ts=range(1))
-    per_slice = time.perf_counter() - t0
-    m = int(max(1, min(T, (0.25 * budget_s) / max(2.0 * per_slice, 1e-6))))
-    t0 = time.perf_counter()
-    O.expected_loglik(Y, Xm, Xc, params, "good", ts=range(m))
-    t_ll = (time.perf_counter() - t0) / m * T
-    t0 = time.perf_counter()
-    off = ~np.eye(n, dtype=bool)
-    for t in range(m):
-        mu = O.compute_mean(Xm[:, t].astype(np.float64), (d - 2) // 2)
-        float((((Y[:, :, t] - mu) ** 2)[off]).sum())
-    t_rec = (time.perf_counter() - t0) / m * T
-    kn = min(n, 64)
-    t0 = time.perf_counter()
-    O.entropy(Xc[:kn])
-    O.log_prior_transitions(Xm[:kn], Xc[:kn], params)
-    O.log_prior_initial(Xm[:kn], Xc[:kn], params)
-    t_node_terms = (time.perf_counter() - t0) / kn * n
-    it_est = sweep_est + t_ll + t_rec + t_node_terms
     units = T * n * (n - 1) / 2.0
+    # --- statistics-form oracle: one full iteration ---
+    Xm, Xc = X32.astype(np.float64), C32.astype(np.float64)
+    k0 = min(n, 16)
+    t0 = time.perf_counter()
+    O.sweep_stats(Y, Xm, Xc, params, "good", 0.01, nodes=range(k0))
+    t_head = time.perf_counter() - t0
+    est = t_head / k0 * n
+    if k0 < n and est <= budget_s:
+        t0 = time.perf_counter()
+        O.sweep_stats(Y, Xm, Xc, params, "good", 0.01, nodes=range(k0, n))
+        t_sweep = t_head + time.perf_counter() - t0
+        swept = n
+    else:
+        t_sweep, swept = est, k0
+    mT = T if n * n * T <= (1 << 28) else max(1, (1 << 28) // (n * n))
+    t0 = time.perf_counter()
+    O.elbo_recon_fast(Y[:, :, :mT], Xm[:, :mT], Xc[:, :mT], params, "good")
+    t_elbo = (time.perf_counter() - t0) * T / mT
+    it_s = t_sweep + t_elbo
+    full = swept == n and mT == T
+    # --- direct restatement: a node sample of the sweep, extrapolated ---
+    Xd, Cd = X32.copy(), C32.copy()
+    consts = O.prior_terms(params, T, np.float32)
+    t0 = time.perf_counter()
+    O.update_node(Y, Xd, Cd, params, 0, "good", 0.01, consts)
+    per_node = time.perf_counter() - t0
+    kd = int(max(1, min(n - 1, (0.15 * budget_s) / max(per_node, 1e-6))))
+    t0 = time.perf_counter()
+    for i in range(1, 1 + kd):
+        O.update_node(Y, Xd, Cd, params, i, "good", 0.01, consts)
+    direct_sweep = (time.perf_counter() - t0) / kd * n
+    direct_it = direct_sweep + t_elbo
     # --- loop-structured restatement: exact-size sample of update steps and pairs ---
     Yt = torch.from_numpy(Y)
-    Xm_t, Xc_t = torch.from_numpy(Xm), torch.from_numpy(Xc)
-    lb = 0.15 * budget_s
+    Xm_t, Xc_t = torch.from_numpy(X32.copy()), torch.from_numpy(C32.copy())
+    lb = 0.08 * budget_s
     t0 = time.perf_counter()
     LO.update_node_loop(Yt, Xm_t, Xc_t, params, n - 1, "good", 0.01, ts=range(1))
     per_step = time.perf_counter() - t0
@@ -129,11 +155,10 @@ def cpu_baseline(model, vi, n, T, d, budget_s=24.0):
     LO.update_node_loop(Yt, Xm_t, Xc_t, params, n - 1, "good", 0.01, ts=range(1, 1 + ns))
     per_step = (time.perf_counter() - t0) / ns
     rng = np.random.default_rng(0)
-    npairs = 2000
-    t0 = time.perf_counter()
     sample = [(int(a), int(b)) for a, b in (sorted(rng.choice(n, 2, replace=False))
-                                            for _ in range(npairs))]
-    LO.loglik_pairs_loop(Yt, Xm_t, Xc_t, params, "good", 0, pairs=sample[:200])
+                                            for _ in range(200))]
+    t0 = time.perf_counter()
+    LO.loglik_pairs_loop(Yt, Xm_t, Xc_t, params, "good", 0, pairs=sample)
     per_pair = (time.perf_counter() - t0) / 200
     npairs = int(max(200, min(200000, lb / max(per_pair, 1e-9))))
     sample = [(int(a), int(b)) for a, b in (sorted(rng.choice(n, 2, replace=False))
@@ -141,14 +166,25 @@ def cpu_baseline(model, vi, n, T, d, budget_s=24.0):
     t0 = time.perf_counter()
     LO.loglik_pairs_loop(Yt, Xm_t, Xc_t, params, "good", 0, pairs=sample)
     per_pair = (time.perf_counter() - t0) / npairs
-    loop_it = per_step * n * T + per_pair * units + t_rec + t_node_terms
+    loop_it = per_step * n * T + per_pair * units + t_elbo
+    how = ("one full iteration measured (no extrapolation)" if full else
+           f"sweep timed on {swept} of {n} nodes, loglik / MSE on {mT} of {T} slices, "
+           "extrapolated linearly")
     return {
-        "value": units / it_est, "unit": UNIT, "cores": int(threads), "kind": "port",
-        "sample": (f"numpy oracle (oracle/ame_oracle.py) fp32, {threads} BLAS threads: "
-                   f"update_node for {k + 1} of {n} nodes x {T} slices, loglik+MSE for {m} of "
-                   f"{T} slices, entropy/prior terms for {kn} nodes; extrapolated linearly to "
-                   f"one full iteration (est. {it_est:.1f} s/iteration)"),
+        "value": units / it_s, "unit": UNIT, "cores": int(threads), "kind": "port",
+        "full_iteration": full, "s_per_iteration": it_s,
+        "sample": (f"numpy oracle, statistics form (oracle/ame_oracle.py sweep_stats + "
+                   f"elbo_recon_fast), fp64, {threads} BLAS threads: {how}; sweep {t_sweep:.1f} s "
+                   f"+ ELBO / MSE {t_elbo:.1f} s = {it_s:.1f} s per iteration"),
         **_host_info(),
+        "direct_restatement": {
+            "value": units / direct_it, "unit": UNIT, "cores": int(threads), "kind": "port",
+            "sample": (f"oracle/ame_oracle.py update_node (P_obs / h_obs re-summed over all "
+                       f"nodes at every step, as the reference), fp32: {kd + 1} of {n} nodes x "
+                       f"{T} slices, extrapolated (sweep est. {direct_sweep:.1f} s) + the "
+                       f"ELBO / MSE above"),
+            "committed_full_iterations": _committed_full_iteration(n, T, r),
+        },
         "loop_restatement": {
             "value": units / loop_it, "unit": UNIT, "cores": 1, "kind": "port",
             "sample": (f"oracle/ame_loop_oracle.py (reference cost model: a torch op sequence "
@@ -183,16 +219,46 @@ def isolated_ms(eng, reps=5):
 
 
 def load_pmc(tag):
-    path = os.path.join(ROOT, "profiles", "pmc_latest.json")
-    if not os.path.exists(path):
-        return None
+    """The committed PMC summary (tools/pmc_summary.py) whose config_tag is this
+    shape: profiles/pmc_latest.json (config 3) or profiles/pmc_latest_*.json."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_latest*.json"))):
+        try:
+            z = json.load(open(path))
+        except Exception:
+            continue
+        if z.get("config_tag") == tag:
+            z["_file"] = os.path.relpath(path, ROOT)
+            return z
+    return None
+
+
+def scaling_model(n, T_total, world, depth, pipelined):
+    """DESIGN.md §5 queue-depth model: node steps per iteration at this world
+    size, against one GPU's n (predicted weak-scaling efficiency = n / that).
+    Pipelined: max(n + hop, (F (T_total - 1) + n + delta) / (1 + depth));
+    in order: the fill F (T_total - 1) + n every iteration."""
+    sys.path.insert(0, os.path.join(ROOT, "python-temporal-ame-svi_amd"))
+    from ame_amd.engine import ELBO_READ_STEPS, FILL_STEPS_PER_SLICE
+    hop = world - 1          # about one node step per rank boundary
+    fill = FILL_STEPS_PER_SLICE * (T_total - 1)
+    if pipelined:
+        steps = max(n + hop, (fill + n + ELBO_READ_STEPS) / (1 + depth))
+        one = max(n, (FILL_STEPS_PER_SLICE * (T_total // world - 1) + n + ELBO_READ_STEPS) / (1 + depth))
+    else:
+        steps = fill + n
+        one = FILL_STEPS_PER_SLICE * (T_total // world - 1) + n
+    return {"node_steps_per_iteration": steps, "one_gpu_node_steps": one,
+            "predicted_efficiency_vs_1gpu": one / steps, "spec_depth": depth,
+            "fill_steps_per_slice": FILL_STEPS_PER_SLICE}
+
+
+def _lib_provenance():
     try:
-        z = json.load(open(path))
-        if z.get("config_tag") != tag:
-            return None
-        return z
-    except Exception:
-        return None
+        from ame_amd import _lib
+        return _lib.provenance()
+    except Exception as e:  # pragma: no cover
+        return {"error": str(e)}
 
 
 def main():
@@ -211,7 +277,10 @@ def main():
     ap.add_argument("--variant", default="good", choices=["good", "bad", "naive"])
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=24.0)
+    ap.add_argument("--cpu-budget", type=float, default=40.0)
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="sweeps in order (profiling: per-dispatch counters without the "
+                         "pipelined launches' waiting)")
     ap.add_argument("--force-dist", action="store_true",
                     help="use the process group (nccl) and the time-sharded path even at world size 1 "
                          "(checks RCCL initialisation on a one-GPU box)")
@@ -238,12 +307,13 @@ def main():
     T_total = args.t_per_gpu * world
     model = TemporalAMEModel(n, T_total, r, seed=42)
     model.generate_data_fast(device=dev)
+    opts = {"pipeline": False} if args.no_pipeline else None
     if args.variant == "naive":
         vi = TemporalAMENaiveMFVI(model, learning_rate=args.lr, device=dev,
-                                  distributed=use_dist)
+                                  distributed=use_dist, engine_options=opts)
     else:
         vi = TemporalAMEStructuredMFVI(model, factorization=args.variant, learning_rate=args.lr,
-                                       device=dev, distributed=use_dist)
+                                       device=dev, distributed=use_dist, engine_options=opts)
     if args.warmup > 0:
         vi.fit(max_iter=args.warmup, tolerance=0.0, verbose=False)
     eng = vi.engine
@@ -260,8 +330,12 @@ def main():
     hist = vi.fit(max_iter=args.steps, tolerance=0.0, verbose=False)
     barrier()
     dt = time.perf_counter() - t0
+    per_rank_ms = [dt / args.steps * 1e3]
     if use_dist:
         tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        allt = [torch.zeros_like(tt) for _ in range(world)]
+        dist.all_gather(allt, tt)
+        per_rank_ms = [float(x.item()) / args.steps * 1e3 for x in allt]
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     kms, kcount = eng.kernel_ms()
@@ -273,7 +347,8 @@ def main():
     b_iter = 8.0 * n * (n - 1) * T_total + 4.0 * n * (n - 1) * T_total \
         + 12.0 * n * T_total * d * d + 16.0 * n * T_total * d
     tag = f"n{n}_T{args.t_per_gpu}_r{r}_{args.variant}"
-    pmc = (load_pmc(tag) or {}).get("kernels", {})
+    pmc_all = load_pmc(tag) or {}
+    pmc = pmc_all.get("kernels", {})
     # cov / elbo launches once more, alone on the GPU (after the timed region)
     iso = isolated_ms(eng)
     pipelined = bool(getattr(eng, "pipelined", False))
@@ -292,13 +367,26 @@ def main():
         if ms:
             ach = kb[name] / (ms * 1e-3) / 1e9
             ent.update(achieved_GBs=ach, frac=ach / HBM_PEAK_GBS)
+        if name == "sweep" and kms.get("sweep"):
+            # the same bytes over the launch's own HIP-event duration (the rocprof
+            # kernel-statistics basis): a pipelined launch's span includes waiting
+            # for the previous sweep's slices, so this is the lower of the two
+            ent["frac_per_launch"] = kb[name] / (kms["sweep"] * 1e-3) / 1e9 / HBM_PEAK_GBS
+            ent["frac_basis"] = {"frac": "algorithmic bytes / ms_per_step (one sweep retires "
+                                         "per iteration)",
+                                 "frac_per_launch": "algorithmic bytes / launch_ms_in_fit "
+                                                    "(HIP events around each launch)"}
         pk = pmc.get({"elbo": "pairs"}.get(name, name))   # elbo: its dominant (pair) kernel
         if pk:
             ent["traffic"] = pk.get("hbm_bytes_per_launch")
             ent["traffic_kernel"] = pk.get("kernel")
+            ent["traffic_source"] = pmc_all.get("_file")
             if ent["traffic"]:
                 alg = kb[name] if name != "elbo" else pk.get("alg_bytes", kb[name])
                 ent["traffic_over_alg"] = ent["traffic"] / alg
+            if name == "pairs" and pk.get("mfma_busy") is not None:
+                ent["mfma_busy"] = pk["mfma_busy"]
+                ent["mfma_method"] = pk.get("mfma_method")
         kernels[name] = ent
     sw = kernels["sweep"]
 
@@ -338,6 +426,10 @@ def main():
             "kernels": kernels,
             "schedule": {"pipelined": pipelined,
                          "sweeps_queued_ahead": int(getattr(eng, "spec_depth", 1))},
+            "per_rank_ms_per_step": per_rank_ms,
+            "scaling_model": scaling_model(n, T_total, world, int(getattr(eng, "spec_depth", 1)),
+                                           pipelined),
+            "build": _lib_provenance(),
             "iteration_roofline_frac": b_iter / (dt / args.steps) / (world * HBM_PEAK_GBS * 1e9),
             "cpu_baseline": cpu,
             "elbo_last": elbo_last,

@@ -235,6 +235,17 @@ int ame_peer_alloc(unsigned long long bytes, void** dev, void* handle);
 int ame_peer_free(void* dev);
 int ame_peer_open(const void* handle, void** dev);
 int ame_peer_close(void* dev);
+/* Setup-time pre-flight of one peer link (no sweep involved): ame_peer_probe
+ * stores `value` into the first 8 bytes of a MAPPED neighbour buffer from a
+ * one-lane kernel on the caller's device (system-scope store + release, the
+ * store the sweep's hand-off uses) and waits for it; ame_peer_read_u64 copies
+ * the first 8 bytes of an OWNED buffer to the host; ame_peer_clear zeroes an
+ * owned buffer again (sentinels must never look like a sweep epoch).  A rank
+ * pair whose probe value does not arrive is named before the first sweep
+ * instead of the sweep spinning into AME_STATUS_HALO_TIMEOUT. */
+int ame_peer_probe(void* peer_dev, unsigned long long value);
+int ame_peer_read_u64(const void* own_dev, unsigned long long* out);
+int ame_peer_clear(void* own_dev, unsigned long long bytes);
 
 /* ---- post-fit alignment -------------------------------
  * Replaces the per-time-step loops of src/utils/alignment.py:

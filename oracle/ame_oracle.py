@@ -197,6 +197,114 @@ def sweep(Y, X_mean, X_cov, params, variant, lr, nodes=None):
 
 
 # ----------------------------------------------------------------------------
+# the same sweep from running sufficient statistics, for
+# parity at the BASELINE shapes
+# ----------------------------------------------------------------------------
+def _slice_stats(M, r):
+    """Per-slice sums over nodes of (U, V) terms: M is (T, n, 2r) current (U, V).
+    Returns [count, sU, sV, S_UU, S_VV, S_VU] with S_VU = sum_j V_j U_j^T."""
+    U, V = M[:, :, :r], M[:, :, r:]
+    Ut, Vt = np.swapaxes(U, 1, 2), np.swapaxes(V, 1, 2)
+    return [np.full(M.shape[0], float(M.shape[1])), U.sum(1), V.sum(1),
+            np.matmul(Ut, U), np.matmul(Vt, V), np.matmul(Vt, U)]
+
+
+def _p_obs(st, R_inv, r):
+    """P_obs of structured_mf.py:303-324 from the statistics (App. A): with
+    e0 = [1, 0, V, 0], e1 = [0, 1, 0, U],
+    P = p e0e0^T + q e0e1^T + q' e1e0^T + s e1e1^T summed over the nodes in st."""
+    m, sU, sV, SUU, SVV, SVU = st
+    T = m.shape[0]
+    d = 2 + 2 * r
+    p, q, q2, s = R_inv[0, 0], R_inv[0, 1], R_inv[1, 0], R_inv[1, 1]
+    A, B, Ub, Vb = 0, 1, slice(2, 2 + r), slice(2 + r, d)
+    P = np.zeros((T, d, d))
+    P[:, A, A] = p * m
+    P[:, A, Ub] = p * sV
+    P[:, Ub, A] = p * sV
+    P[:, Ub, Ub] = p * SVV
+    P[:, A, B] = q * m
+    P[:, A, Vb] = q * sU
+    P[:, Ub, B] = q * sV
+    P[:, Ub, Vb] = q * SVU
+    P[:, B, A] += q2 * m
+    P[:, Vb, A] = q2 * sU
+    P[:, B, Ub] += q2 * sV
+    P[:, Vb, Ub] = q2 * np.swapaxes(SVU, 1, 2)
+    P[:, B, B] = s * m
+    P[:, B, Vb] += s * sU
+    P[:, Vb, B] = s * sU
+    P[:, Vb, Vb] = s * SUU
+    return P
+
+
+def sweep_stats(Y, X_mean, X_cov, params, variant, lr, nodes=None):
+    """_update_step (structured_mf.py:211-287, naive_mf.py:207-282) in fp64, in
+    place, vectorised over time: the same Gauss-Seidel node order and the same
+    per-step formulas as :func:`update_node`, but P_obs / h_obs come from
+    per-slice running sums of the other nodes' (U, V) and
+    everything that does not depend on mu_{i,t-1}^new is batched over t (P,
+    its inverse, the right AR term); only mu_{i,t} = C_t (h_t + Q^-1 Phi
+    mu_{i,t-1}) runs as a loop.  Pinned to :func:`sweep` in
+    tests/test_oracle_fast.py; used where the direct restatement is too slow
+    (full sweeps at n = 1024-4096)."""
+    n, T, d = X_mean.shape
+    r = (d - 2) // 2
+    assert X_mean.dtype == np.float64 and X_cov.dtype == np.float64
+    R_inv = params["R_inv"].astype(np.float64)
+    Q_inv, S0_inv, PtQiP = prior_terms({k: v.astype(np.float64) for k, v in params.items()},
+                                       T, np.float64)
+    Phi = params["Phi"].astype(np.float64)
+    QiPhi = Q_inv @ Phi
+    PhiTQi = Phi.T @ Q_inv
+    eye = np.eye(d)
+    M = np.ascontiguousarray(np.swapaxes(X_mean[:, :, 2:], 0, 1))      # (T, n, 2r) current
+    st = _slice_stats(M, r)
+    for i in (range(n) if nodes is None else nodes):
+        own = M[:, i, :]                                                 # (T, 2r) old
+        Uo, Vo = own[:, :r], own[:, r:]
+        ex = [st[0] - 1.0, st[1] - Uo, st[2] - Vo,
+              st[3] - np.einsum("ta,tb->tab", Uo, Uo), st[4] - np.einsum("ta,tb->tab", Vo, Vo),
+              st[5] - np.einsum("ta,tb->tab", Vo, Uo)]
+        P = _p_obs(ex, R_inv, r)
+        yi = np.asarray(Y[i], dtype=np.float64).transpose(1, 2, 0)     # (T, 2, n)
+        z = np.matmul(R_inv, yi)                                        # z_ij = R^-1 y_ij
+        z[:, :, i] = 0.0                                                # j != i
+        zM = np.matmul(z, M)                                            # (T, 2, 2r)
+        h = np.empty((T, d))
+        h[:, :2] = z.sum(2)
+        h[:, 2:2 + r] = zM[:, 0, r:]                                    # sum z0 V_j
+        h[:, 2 + r:] = zM[:, 1, :r]                                     # sum z1 U_j
+        P[0] += S0_inv
+        P[1:] += Q_inv
+        P[:-1] += PtQiP
+        if T > 1:
+            h[:-1] += X_mean[i, 1:] @ PhiTQi.T                          # old mu_{i,t+1}
+        Pinv = np.linalg.inv(P)
+        if variant == "naive":
+            C = np.zeros_like(P)
+            idx = np.arange(d)
+            C[:, idx, idx] = 1.0 / (P[:, idx, idx] + 1e-8)
+            G = Pinv
+        else:
+            C = Pinv.copy()
+            if variant == "bad":
+                C[:, :2, 2:] = 0.0
+                C[:, 2:, :2] = 0.0
+            C = (C + np.swapaxes(C, 1, 2)) / 2.0 + eye * 1e-6
+            G = C
+        for t in range(T):
+            ht = h[t] + (QiPhi @ X_mean[i, t - 1] if t > 0 else 0.0)
+            X_mean[i, t] = lr * (G[t] @ ht) + (1.0 - lr) * X_mean[i, t]
+        X_cov[i] = lr * C + (1.0 - lr) * X_cov[i]
+        new = X_mean[i, :, 2:]
+        Un, Vn = new[:, :r], new[:, r:]
+        st = [st[0], ex[1] + Un, ex[2] + Vn, ex[3] + np.einsum("ta,tb->tab", Un, Un),
+              ex[4] + np.einsum("ta,tb->tab", Vn, Vn), ex[5] + np.einsum("ta,tb->tab", Vn, Un)]
+        M[:, i, :] = new
+
+
+# ----------------------------------------------------------------------------
 # ELBO (structured_mf.py:115-209; naive_mf.py:89-191) and recon
 # (temporal_ame.py:255-291)
 # ----------------------------------------------------------------------------
@@ -292,6 +400,51 @@ def recon_error(Y, X_mean):
         e = (Y[:, :, t].astype(np.float64) - mu) ** 2
         tot += float(e[off].sum())
     return tot / (n * (n - 1) * T)
+
+
+def elbo_recon_fast(Y, X_mean, X_cov, params, variant):
+    """elbo_split + recon_error of the same state, vectorised per slice in fp64
+    (whole n x n residual matrices instead of index gathers; the entropy's
+    log-determinants batched).  Same formulas as above (structured_mf.py:124-209,
+    naive_mf.py:114-191, temporal_ame.py:255-291); pinned to them in
+    tests/test_oracle_fast.py.  Returns (split[4], recon)."""
+    n, T, d = X_mean.shape
+    r = (d - 2) // 2
+    R_inv = params["R_inv"].astype(np.float64)
+    p, q, q2, s = R_inv[0, 0], R_inv[0, 1], R_inv[1, 0], R_inv[1, 1]
+    logdetR = _logdet(params["R"])
+    trRi = float(np.trace(R_inv))
+    upper = np.triu(np.ones((n, n), dtype=bool), k=1)
+    off = ~np.eye(n, dtype=bool)
+    quad_sum = 0.0
+    sq_sum = 0.0
+    CH = 8                                    # slices per gather: whole cache lines of Y
+    for t in range(T):
+        if t % CH == 0:
+            yc = np.ascontiguousarray(np.moveaxis(Y[:, :, t:t + CH, :], 2, 0), dtype=np.float64)
+        x = X_mean[:, t].astype(np.float64)
+        add = x[:, 0][:, None] + x[:, 1][None, :]
+        mult = x[:, 2:2 + r] @ x[:, 2 + r:].T
+        m0 = add + mult                       # mean of y_ij[0]
+        yt = yc[t % CH]
+        e0 = yt[:, :, 0] - m0
+        e1 = yt[:, :, 1] - m0.T
+        quad = p * e0 * e0 + (q + q2) * e0 * e1 + s * e1 * e1
+        quad_sum += float(quad[upper].sum())
+        sq_sum += float((e0 * e0 + e1 * e1)[off].sum())
+    npairs = T * n * (n - 1) / 2.0
+    if variant == "naive":
+        corr = 0.0
+    else:
+        tr = np.trace(X_cov.astype(np.float64), axis1=2, axis2=3)      # (n, T)
+        corr = 0.1 * trRi / d * (n - 1) * float(tr.sum())
+    loglik = -0.5 * (npairs * (logdetR + 2 * LOG2PI) + quad_sum + corr)
+    sign, ld = np.linalg.slogdet(X_cov.astype(np.float64).reshape(-1, d, d))
+    ld = np.where(sign > 0, ld, np.where(sign == 0, -np.inf, np.nan))
+    ent = float(np.sum(0.5 * (d * (1 + LOG2PI) + ld)))
+    split = np.array([loglik, log_prior_initial(X_mean, X_cov, params),
+                      log_prior_transitions(X_mean, X_cov, params), ent])
+    return split, sq_sum / (n * (n - 1) * T)
 
 
 # ----------------------------------------------------------------------------

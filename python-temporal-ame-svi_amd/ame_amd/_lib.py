@@ -57,6 +57,7 @@ class ame_elbo_args(ctypes.Structure):
 EXPORTS = ("ame_pack_y", "ame_pack_y_size", "ame_sweep", "ame_sweep_kind", "ame_sweep_work_size", "ame_sweep_orders_slices", "ame_sweep_max_slices", "ame_sweep_lds_bytes", "ame_cov",
            "ame_elbo", "ame_elbo_work_size", "ame_elbo_pairs_diag", "ame_host_register", "ame_host_unregister",
            "ame_peer_alloc", "ame_peer_free", "ame_peer_open", "ame_peer_close",
+           "ame_peer_probe", "ame_peer_read_u64", "ame_peer_clear",
            "ame_supported_r", "ame_last_error", "ame_version", "ame_align_work_size",
            "ame_align_cross_size", "ame_align_partials_size", "ame_align_cross", "ame_align_apply")
 
@@ -96,6 +97,9 @@ def _declare(L):
     L.ame_peer_free.argtypes = [c_vp]
     L.ame_peer_open.argtypes = [c_vp, P(c_vp)]
     L.ame_peer_close.argtypes = [c_vp]
+    L.ame_peer_probe.argtypes = [c_vp, ctypes.c_ulonglong]
+    L.ame_peer_read_u64.argtypes = [c_vp, P(ctypes.c_ulonglong)]
+    L.ame_peer_clear.argtypes = [c_vp, ctypes.c_ulonglong]
     ci = ctypes.c_int
     for name in ("ame_align_work_size", "ame_align_cross_size"):
         getattr(L, name).restype = ctypes.c_longlong
@@ -111,7 +115,8 @@ def _declare(L):
     L.ame_version.restype = ctypes.c_char_p
     for name in ("ame_pack_y", "ame_sweep", "ame_cov", "ame_elbo", "ame_sweep_max_slices",
                  "ame_supported_r", "ame_host_register", "ame_host_unregister", "ame_peer_alloc",
-                 "ame_peer_free", "ame_peer_open", "ame_peer_close"):
+                 "ame_peer_free", "ame_peer_open", "ame_peer_close", "ame_peer_probe",
+                 "ame_peer_read_u64", "ame_peer_clear"):
         getattr(L, name).restype = ctypes.c_int
     return L
 
@@ -136,6 +141,25 @@ def check(rc, what):
     if rc != 0:
         msg = lib().ame_last_error().decode(errors="replace")
         raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+
+def build_hash():
+    """The source hash the loaded library was built from (ame_version "src=")."""
+    v = lib().ame_version().decode(errors="replace")
+    return v.split("src=", 1)[1] if "src=" in v else None
+
+
+def provenance():
+    """{lib, tree, match}: the loaded library's source hash against the hash of
+    the sources beside it (ame_amd/build.py), so a stale library is visible."""
+    from .build import source_hash
+    got = build_hash()
+    try:
+        tree = source_hash()
+    except OSError:   # pragma: no cover - sources not shipped
+        tree = None
+    return {"lib_src": got, "tree_src": tree, "match": got is not None and got == tree,
+            "path": LIB_PATH}
 
 
 def supported_r():

@@ -5,7 +5,9 @@
 from __future__ import annotations
 
 import concurrent.futures as cf
+import hashlib
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -43,31 +45,85 @@ def _hipcc():
     raise RuntimeError("hipcc not found (ROCm required to build ame_amd)")
 
 
-def _stale(objs):
-    if not os.path.exists(OUT):
-        return True
-    t = os.path.getmtime(OUT)
-    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
-    deps.append(os.path.join(HERE, "..", "..", "include", "ame_amd.h"))
-    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+FLAGS = [f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-pass-failed"]
+_VERSION_RE = re.compile(rb"ame_amd 0\.\d+ gfx950 src=([0-9a-f]{16}|unknown)")
+
+
+def _inputs():
+    """Every file the library is built from: csrc/* and the C-ABI header."""
+    files = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC)
+                   if f.endswith((".hip", ".h")))
+    files.append(os.path.join(HERE, "..", "..", "include", "ame_amd.h"))
+    return [f for f in files if os.path.exists(f)]
+
+
+def source_hash() -> str:
+    """SHA-256 prefix over the sources, headers, flags and split layout: what
+    ame_version() of a library built from this tree reports after "src="."""
+    h = hashlib.sha256()
+    h.update(repr((FLAGS, sorted(SPLIT.items()), SOURCES)).encode())
+    for f in _inputs():
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def embedded_hash(path: str = OUT):
+    """The src= hash compiled into a built library (read from the file, not
+    loaded), or None."""
+    if not os.path.exists(path):
+        return None
+    with open(path, "rb") as fh:
+        m = _VERSION_RE.search(fh.read())
+    return m.group(1).decode() if m else None
+
+
+def _unit_key(src, extra, headers_digest, src_hash):
+    h = hashlib.sha256()
+    with open(os.path.join(CSRC, src), "rb") as fh:
+        h.update(fh.read())
+    h.update(headers_digest.encode())
+    h.update(repr((FLAGS, extra)).encode())
+    if src == "ame_capi.hip":
+        h.update(src_hash.encode())
+    return h.hexdigest()
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
+    """Rebuild when the library's embedded source hash differs from the tree's
+    (content, not mtimes); objects whose inputs did not change are reused."""
+    src_hash = source_hash()
+    if not force and embedded_hash(OUT) == src_hash:
+        return OUT
     hipcc = _hipcc()
     bdir = os.path.join(HERE, "_build")
     os.makedirs(bdir, exist_ok=True)
     units = _units()
     objs = [os.path.join(bdir, o) for _, o, _ in units]
-    if not force and not _stale(objs):
-        return OUT
-    flags = [f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-pass-failed"]
+    hd = hashlib.sha256()
+    for f in _inputs():
+        if f.endswith(".h"):
+            with open(f, "rb") as fh:
+                hd.update(fh.read())
+    headers_digest = hd.hexdigest()
 
     def compile_one(unit):
         src, obj, extra = unit
-        cmd = [hipcc, *flags, *extra, "-c", os.path.join(CSRC, src), "-o", os.path.join(bdir, obj)]
+        if src == "ame_capi.hip":
+            extra = [*extra, f'-DAME_SRC_HASH="{src_hash}"']
+        key = _unit_key(src, extra, headers_digest, src_hash)
+        opath = os.path.join(bdir, obj)
+        kpath = opath + ".key"
+        if not force and os.path.exists(opath) and os.path.exists(kpath) \
+                and open(kpath).read() == key:
+            return obj
+        cmd = [hipcc, *FLAGS, *extra, "-c", os.path.join(CSRC, src), "-o", opath]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src} {extra}:\n{r.stderr[-4000:]}")
+        with open(kpath, "w") as fh:
+            fh.write(key)
         return obj
 
     jobs = min(len(units), max(1, min(16, os.cpu_count() or 1)))
@@ -81,9 +137,12 @@ def build(force: bool = False, verbose: bool = True) -> str:
                        capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
+    got = embedded_hash(tmp)
+    if got != src_hash:
+        raise RuntimeError(f"built library reports src={got}, tree is {src_hash}")
     os.replace(tmp, OUT)
     if verbose:
-        print(f"built {OUT}", file=sys.stderr)
+        print(f"built {OUT} (src={src_hash})", file=sys.stderr)
     return OUT
 
 

@@ -64,7 +64,13 @@ extern "C" {
 
 const char* ame_last_error(void) { return g_err; }
 
-const char* ame_version(void) { return "ame_amd 0.3 gfx950"; }
+// AME_SRC_HASH: SHA-256 prefix of every source, header and build flag that
+// went into this library (ame_amd/build.py source_hash()); build() compares it
+// with the tree and rebuilds on a mismatch, and tests / bench report it
+#ifndef AME_SRC_HASH
+#define AME_SRC_HASH "unknown"
+#endif
+const char* ame_version(void) { return "ame_amd 0.4 gfx950 src=" AME_SRC_HASH; }
 
 // test hook (not in the header): the GEMV-worker partial tag (ame_common.h)
 unsigned int ame_debug_gw_tag(unsigned int epoch, int m) { return ame_gw_tag(epoch, m); }
@@ -133,6 +139,47 @@ int ame_peer_open(const void* handle, void** dev) {
 int ame_peer_close(void* dev) {
     if (!dev) return fail("ame_peer_close: NULL");
     return hipIpcCloseMemHandle(dev) == hipSuccess ? 0 : fail("ame_peer_close failed");
+}
+
+__global__ void ame_peer_probe_kernel(unsigned long long* dst, unsigned long long v) {
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    }
+}
+
+int ame_peer_probe(void* peer_dev, unsigned long long value) {
+    if (!peer_dev) return fail("ame_peer_probe: NULL");
+    hipLaunchKernelGGL(ame_peer_probe_kernel, dim3(1), dim3(64), 0, 0,
+                       (unsigned long long*)peer_dev, value);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+        snprintf(g_err, sizeof(g_err), "ame_peer_probe: %s", hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+}
+
+int ame_peer_read_u64(const void* own_dev, unsigned long long* out) {
+    if (!own_dev || !out) return fail("ame_peer_read_u64: NULL");
+    hipError_t e = hipMemcpy(out, own_dev, sizeof(*out), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+        snprintf(g_err, sizeof(g_err), "ame_peer_read_u64: %s", hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+}
+
+int ame_peer_clear(void* own_dev, unsigned long long bytes) {
+    if (!own_dev || bytes == 0) return fail("ame_peer_clear: bad arguments");
+    hipError_t e = hipMemset(own_dev, 0, (size_t)bytes);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+        snprintf(g_err, sizeof(g_err), "ame_peer_clear: %s", hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
 }
 
 static int device_cus() {

@@ -514,11 +514,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
 #pragma unroll
         for (int r = 0; r < AME_YPF; ++r) {
             const int j = tid + AME_NT * r;
-#ifdef AME_ABL_NOY
-            ypf[r] = make_float2((float)j, 0.f); (void)yrow;
-#else
             ypf[r] = (j < n) ? yrow[j] : make_float2(0.f, 0.f);
-#endif
         }
     };
     auto stage_z = [&](int node, int excl) {   // z row of `node` from ypf (+ tail loads)

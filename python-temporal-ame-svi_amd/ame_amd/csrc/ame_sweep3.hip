@@ -110,10 +110,7 @@ constexpr int kNH = 448;    // helper lanes
 // hw 0-1, whose HB + HF1 + GEMV chain is the longest of the step.  Measured at
 // config 3 (profiles/r02_goff.txt): offset 192 (hw 3-4) and 320 (hw 5-6) are
 // no faster (2.75 / 2.77 vs 2.74 ms per iteration), so 0 stays.
-#ifndef AME_S3_GOFF
-#define AME_S3_GOFF 0
-#endif
-constexpr int kGOFF = AME_S3_GOFF;
+constexpr int kGOFF = 0;
 constexpr int kMREG = 96;   // VGPR budget for the register-resident part of the node slice
 constexpr int kLDSMAX = 160 * 1024;
 
@@ -196,11 +193,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     const bool is_naive = dm.variant == AME_NAIVE, is_bad = dm.variant == AME_BAD;
     const int ns = (n + kNH - 1) / kNH;
     const int NY = (n * 8 + 1023) / 1024;     // DMA KiB per Y row
-#ifdef AME_S3_OLDP
-    const int KDMA = NY + NC + 3;
-#else
     const int KDMA = NY + NC + 2;             // DMA instructions per step (loader wave)
-#endif
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     using LY = Lay<R>;
@@ -317,13 +310,6 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         const float* src = (xr != nullptr && node < n) ? xr + (size_t)node * D : xo;
         if (back_rd) dma4_sys(src + (lane < D ? lane : 0), lds_off(rring + (node & 3) * 64));
         else dma4(src + (lane < D ? lane : 0), lds_off(rring + (node & 3) * 64));
-    };
-    auto dma_p = [&](int node) {   // granules of mu_{node, t-1} -> slot node & 3 : 1 instruction
-        const uint32_t dst = lds_off(pring + (size_t)(node & 3) * 128);
-        const int g2 = (lane * 2 < D) ? lane * 2 : 0;
-        if (tg == 0 || node >= n) dma16(xo, dst);
-        else if (tl == 0) dma16_sys(gran_src(node) + g2, dst);
-        else dma16_sc1(gran_src(node) + g2, dst);
     };
 
     // staged new covariance of `node` -> cvw, 16 B per lane, whole rows (DD % 4 == 0)
@@ -547,13 +533,11 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 const float z1 = ex ? 0.f : r10f * yv[s].x + r11f * yv[s].y;
                 acc[0] += z0;
                 acc[1] += z1;
-#ifndef AME_ABL_GEMV_NOFMA
 #pragma unroll
                 for (int c = 0; c < R; ++c) {
                     acc[2 + c] = fmaf(z0, mreg[s][R + c], acc[2 + c]);       // h_U += z0 V
                     acc[2 + R + c] = fmaf(z1, mreg[s][c], acc[2 + R + c]);   // h_V += z1 U
                 }
-#endif
             }
         }
         for (int s = NSREG; s < ns; ++s) {
@@ -580,11 +564,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         }
         STAMP3(7);
         int idx;
-#ifndef AME_ABL_GEMV_NORED
         const float v = wave_reduce_scatter<D>(acc, lane, idx);
-#else
-        const float v = acc[lane % D]; idx = lane;
-#endif
         STAMP3(8);
         if (idx < D) gp[((m & 1) * 7 + hw) * D + idx] = v;
         // raw y_{m,m-1}, y_{m,m-2} for the solver / HF1 (owner lanes only)
@@ -669,20 +649,6 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             if (tg > 0 && lane < D)
                 g0 = (tl == 0) ? gran_load_system(gran_src(0) + lane) : gran_load_agent(gran_src(0) + lane);
             gran_finish(0, g0, muL + hw * 64);
-#ifdef AME_S3_LAG
-            // Experiment (off by default): keep slice t at least
-            // AME_S3_LAG + 1 node steps behind slice t-1, so the hand-off granules the
-            // loader DMAs 3 steps ahead of their use are already current and HF1
-            // skips the L2 poll.  Measured: step period unchanged (the loader and HX
-            // waves, not HF1, set it), plus a (AME_S3_LAG + 1)-step fill per slice.
-            if (hw == 0 && tg > 0 && n > 1) {
-                const int lagn = min(n - 1, AME_S3_LAG);
-                uint64_t gl = 0;
-                if (lane < D)
-                    gl = (tl == 0) ? gran_load_system(gran_src(lagn) + lane) : gran_load_agent(gran_src(lagn) + lane);
-                gran_finish(lagn, gl, (float*)red + 64);
-            }
-#endif
         }
         if (hw == 3) jn_fill(1);
     }
@@ -692,26 +658,19 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     if (wave == 7) {   // Y rows 2..4 (slots 2,3,0), covariances of nodes 0,1
         for (int q = 2; q <= 4; ++q) dma_y(q);
         for (int q = 0; q <= 1; ++q) dma_cov(q);
-#ifdef AME_S3_OLDP
-        for (int q = 1; q <= 3; ++q) dma_p(q);
-#endif
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-#ifndef AME_S3_OLDP
     if (wave == 6 && lane < D) {   // granules of node 1 (8-byte atomic loads, see below)
         uint64_t g1 = 0;
         if (tg > 0 && n > 1)
             g1 = (tl == 0) ? gran_load_system(gran_src(1) + lane) : gran_load_agent(gran_src(1) + lane);
         pring[(size_t)1 * 128 + lane] = g1;
     }
-#endif
     __syncthreads();
 
     if (wave == 0) {
         // ============================ SOLVER ============================
-#ifndef AME_ABL_NOPRIO
         __builtin_amdgcn_s_setprio(3);
-#endif
         const int k = lane;
         const bool kl = k < D;
         const int kc = kl ? k : 0;
@@ -901,12 +860,19 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 if (kl) {
                     const float* xold = xring + (i & 7) * 64;
                     const double p = r00, s = r11;
+                    // lane k reads its partner column's sum before any lane
+                    // updates its own: the read is issued first and the compiler
+                    // may not move it past the barrier below (the two addresses
+                    // differ per lane, so without it the store could be hoisted
+                    // above another lane's read of the same word)
+                    const double sq_src = ssq[src];
+                    asm volatile("" ::: "memory");
                     double pd;
                     if (k == 0) pd = p * (double)(n - 1);
                     else if (k == 1) pd = s * (double)(n - 1);
                     else {
                         const double oo = (k < 2 + R) ? (double)xold[k + R] : (double)xold[k - R];
-                        pd = ((k < 2 + R) ? p : s) * (ssq[src] - oo * oo);
+                        pd = ((k < 2 + R) ? p : s) * (sq_src - oo * oo);
                     }
                     pdl[par * D + k] = pd + pcdl[k];
                     const double mo = (double)mold, mn = (double)nw;
@@ -931,9 +897,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             if (i + 1 < n) {   // g_{i+1} and Jn of node i+2 from HF1 (hw 0..2)
                 lds_wait_ge(gcnt, 3u * (uint32_t)(i + 1), a.status, dead);
                 STAMP3(8);
-#ifndef AME_ABL_NOPREP
                 prep(i + 1);
-#endif
                 STAMP3(9);
             }
             lds_barrier3();
@@ -945,10 +909,6 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         lds_barrier3();   // epilogue step n
     } else {
         // ============================ HELPERS ============================
-#ifdef AME_S3_HPRIO
-        // diagnostic: helper waves above the waves of kernels running beside the sweep
-        __builtin_amdgcn_s_setprio(AME_S3_HPRIO);
-#endif
         int lk[LTQ], lm[LTQ];
 #pragma unroll
         for (int q = 0; q < LTQ; ++q) {
@@ -976,7 +936,6 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             // a vmcnt(0) there would also drain the loader's LDS-DMA and hw 4's
             // covariance stores at every step start)
             uint64_t pgr;
-#ifndef AME_S3_OLDP
             if (hw == 5) {
                 if (i + 2 < n && tg > 0 && lane < D)
                     pgr = (tl == 0) ? gran_load_system(gran_src(i + 2) + lane)
@@ -984,7 +943,6 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 else
                     pgr = 0;
             }
-#endif
             // HB (hw 0..5): K_i = B_i - L W^T + G X^T, fused covariance of node i-1
             if (hw <= 5) {
                 const double* rp = rec + (size_t)ppar * D * RS;   // [k][field]
@@ -1015,14 +973,10 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                         Kn[k * KS + m] = kn;
                         Kn[m * KS + k] = kn;
                     }
-#ifndef AME_ABL_NOCOVST
                     if (ok && i >= 1) {
                         cv[k * D + m] = n_km;
-#ifndef AME_ABL_NOTSTORE
                         if (k != m) cv[m * D + k] = n_mk;
-#endif
                     }
-#endif
                 }
             }
             STAMP3(4);
@@ -1066,11 +1020,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                     }
                 }
                 // HE: GEMV of node i+2 (its Y row landed in the ring by step i-1)
-#ifdef AME_ABL_NOGEMV012
-                if (i + 2 < n && hw >= 3) gemv(i + 2, yring + (size_t)((i + 2) & 3) * YS, i);
-#else
                 if (i + 2 < n) gemv(i + 2, yring + (size_t)((i + 2) & 3) * YS, i);
-#endif
                 STAMP3(5);
                 // loader: this step's batch -- Y row i+5, covariance of node i+2, old
                 // means of node i+5 (slice t) and i+4 (slice t+1)
@@ -1079,9 +1029,6 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                     dma_cov(i + 2);
                     dma_x(i + 5);
                     dma_r(i + 4);
-#ifdef AME_S3_OLDP
-                    dma_p(i + 4);
-#endif
                     STAMP3(6);
                 }
             }
@@ -1089,9 +1036,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             if (hw == 6) vm_wait_le(2 * KDMA);
             // granules of node i+2, read by HF1 next step (slot (i+2) & 3: not read
             // this step)
-#ifndef AME_S3_OLDP
             if (hw == 5 && i < n && lane < D) pring[(size_t)((i + 2) & 3) * 128 + lane] = pgr;
-#endif
             STAMP3(9);
             lds_barrier3();
         }

@@ -74,6 +74,13 @@ class PeerBuffer:
             self.handle = handle
             self.owner = False
 
+    def quiesce_local(self, eng):
+        """Exception path of fit(): wait for this rank's own kernels only (no
+        collective: the other ranks may be inside a different one)."""
+        if self._peers is None:
+            return
+        torch.cuda.synchronize(eng.dev)
+
     def close(self):
         if self.dev is None or not self.dev.value:
             return
@@ -96,6 +103,7 @@ class TimeShardHalo:
         self._prev_final = None
         # gloo (CPU tests, several ranks sharing one GPU) needs host staging
         self._host_coll = dist.get_backend(group) == "gloo"
+        self.preflight_ok = False    # set by _preflight once every peer link carried its sentinel
 
     def _coll(self, t: torch.Tensor):
         return t.cpu() if (self._host_coll and t.is_cuda) else t
@@ -131,8 +139,65 @@ class TimeShardHalo:
             peer_halo = PeerBuffer(handle=allh[rank + 1][0]) if rank < world - 1 else None
             peer_back = PeerBuffer(handle=allh[rank - 1][1]) if rank > 0 else None
         self._peers = (own_halo, own_back, peer_halo, peer_back)
-        dist.barrier(group=self.group)
         atexit.register(self.close)
+        self._preflight(eng)
+
+    @staticmethod
+    def _sentinel(kind: int, writer: int, owner: int) -> int:
+        # high word 0xA3E5xxxx: never an epoch the sweep waits for (epochs count
+        # up from 1), and the buffers are zeroed again after the check
+        return ((0xA3E50000 | (kind << 12) | (writer & 0xFFF)) << 32) | (owner & 0xFFFFFFFF)
+
+    def _preflight(self, eng, wait_s: float = 2.0):
+        """Every peer link once, before the first sweep: each rank stores a
+        sentinel into each buffer it MAPPED (the right neighbour's halo, the left
+        neighbour's back channel) with the same system-scope store the sweep's
+        hand-off uses, from its own device; after a barrier every owner reads
+        its buffers back.  A missing or wrong value raises naming the rank pair
+        and the link, instead of the first sweep spinning until the status word
+        reports a halo timeout.  Reference: structured_mf.py:240 (the T loop
+        whose boundary the links carry)."""
+        import time
+        L = _lib.lib()
+        rank = self.shard.rank
+        own_halo, own_back, peer_halo, peer_back = self._peers
+        with torch.cuda.device(eng.dev):
+            if peer_halo is not None:
+                _lib.check(L.ame_peer_probe(peer_halo.dev, self._sentinel(1, rank, rank + 1)),
+                           f"ame_peer_probe (rank {rank} -> halo of rank {rank + 1})")
+            if peer_back is not None:
+                _lib.check(L.ame_peer_probe(peer_back.dev, self._sentinel(2, rank, rank - 1)),
+                           f"ame_peer_probe (rank {rank} -> back channel of rank {rank - 1})")
+        dist.barrier(group=self.group)
+        bad = []
+        with torch.cuda.device(eng.dev):
+            for buf, writer, kind, nbytes, what in (
+                    (own_halo, rank - 1, 1, eng.n * eng.d * 8, "left halo"),
+                    (own_back, rank + 1, 2, self._back_bytes, "back channel")):
+                if buf is None:
+                    continue
+                want = self._sentinel(kind, writer, rank)
+                got = ctypes.c_ulonglong(0)
+                t0 = time.monotonic()
+                while True:
+                    _lib.check(L.ame_peer_read_u64(buf.dev, ctypes.byref(got)), "ame_peer_read_u64")
+                    if got.value == want or time.monotonic() - t0 > wait_s:
+                        break
+                    time.sleep(0.01)
+                if got.value != want:
+                    bad.append(f"rank {writer} -> rank {rank} ({what}): read {got.value:#018x}, "
+                               f"expected {want:#018x}")
+                _lib.check(L.ame_peer_clear(buf.dev, nbytes), "ame_peer_clear")
+        flag = torch.tensor([len(bad)], dtype=torch.int32,
+                            device="cpu" if self._host_coll else eng.dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+        if bad:
+            msg = L.ame_last_error().decode(errors="replace")
+            raise RuntimeError("ame_amd: peer-link pre-flight failed: " + "; ".join(bad) +
+                               f" (last library message: {msg!r})")
+        if int(flag.item()):
+            raise RuntimeError("ame_amd: peer-link pre-flight failed on another rank")
+        self.preflight_ok = True
 
     def quiesce(self, eng):
         """Called by every rank when fit() ends (after the dropped speculative

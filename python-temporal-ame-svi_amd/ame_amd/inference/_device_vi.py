@@ -146,15 +146,28 @@ class DeviceTemporalVI(BaseTemporalVariationalInference):
         # sweeps may be started ahead (bounded by the engine's spec_depth)
         self._spec_next = max(0, max_iter - 1 - iteration)
 
-    def _fit_end(self) -> None:
+    def _fit_end(self, ok: bool = True) -> None:
         self._spec_next = 0
-        if self._engine is not None:
-            self._engine.discard_speculation()
-            halo = getattr(self, "_halo", None)
-            if halo is not None:
-                # no rank leaves fit() while a neighbour's dropped sweep may still
-                # store into its peer buffers (they are freed at close / exit)
-                halo.quiesce(self._engine)
+        if self._engine is None:
+            return
+        halo = getattr(self, "_halo", None)
+        if not ok:
+            # fit() is raising: the peers may sit in a collective this rank never
+            # enters (the ELBO all_reduce, agree()), so no barrier here, and a
+            # faulted device must not replace the original exception.  The peer
+            # buffers stay mapped until close() at exit.
+            try:
+                self._engine.discard_speculation()
+                if halo is not None:
+                    halo.quiesce_local(self._engine)
+            except Exception:
+                pass
+            return
+        self._engine.discard_speculation()
+        if halo is not None:
+            # no rank leaves fit() while a neighbour's dropped sweep may still
+            # store into its peer buffers (they are freed at close / exit)
+            halo.quiesce(self._engine)
 
     def _terms(self):
         return self._ensure_engine().terms(speculate=getattr(self, "_spec_next", 0))

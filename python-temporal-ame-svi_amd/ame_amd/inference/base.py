@@ -46,6 +46,7 @@ class BaseVariationalInference(ABC):
         converged = False
         patience_counter = 0
         prev_elbo = -np.inf
+        ok = False
         try:
             for iteration in range(max_iter):
                 self._fit_iteration(iteration, max_iter)
@@ -69,8 +70,9 @@ class BaseVariationalInference(ABC):
                     if verbose:
                         print(f"\nConverged at iteration {iteration}")
                     break
+            ok = True
         finally:
-            self._fit_end()
+            self._fit_end(ok)
         if verbose and not converged:
             print("\nReached maximum iterations without convergence")
         return self.history
@@ -78,8 +80,8 @@ class BaseVariationalInference(ABC):
     def _fit_iteration(self, iteration: int, max_iter: int) -> None:
         """Hook: fit() is about to run `iteration` of `max_iter` (no-op here)."""
 
-    def _fit_end(self) -> None:
-        """Hook: fit() is returning or raising (no-op here)."""
+    def _fit_end(self, ok: bool = True) -> None:
+        """Hook: fit() is returning (ok) or raising (not ok); no-op here."""
 
     def _compute_reconstruction_error(self) -> float:
         if hasattr(self, "get_variational_means"):

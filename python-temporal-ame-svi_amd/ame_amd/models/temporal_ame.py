@@ -43,6 +43,30 @@ def _block_diag_cov(sizes, corrs, variances) -> torch.Tensor:
     return cov
 
 
+
+def fma_f32(p: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
+    """fp32 fused multiply-add result p + s rounded ONCE to fp32, for p an
+    exact fp64 product of two fp32 values and s fp32.  The fp64 sum is rounded
+    first, so a plain ``.float()`` would round twice; the fp64 rounding error
+    (TwoSum, exact) decides the halfway cases: when the fp64 sum lies exactly
+    midway between two fp32 values and the error is non-zero, the true sum is
+    on the error's side, and the sum is moved one fp64 ulp there before the
+    fp32 rounding (no other fp32 rounding boundary lies within one fp64 ulp)."""
+    s64 = s.double()
+    t = p + s64
+    bp = t - s64
+    err = (p - bp) + (s64 - (t - bp))
+    f = t.float()
+    fd = f.double()
+    toward = torch.where(t > fd, torch.full_like(f, float("inf")), torch.full_like(f, float("-inf")))
+    mid = (fd + torch.nextafter(f, toward).double()) * 0.5
+    tie = (t == mid) & (t != fd) & (err != 0)
+    if bool(tie.any()):
+        step = torch.where(err > 0, torch.full_like(t, float("inf")), torch.full_like(t, float("-inf")))
+        t = torch.where(tie, torch.nextafter(t, step), t)
+        f = t.float()
+    return f
+
 class TemporalAMEModel:
     """Temporal AME model with AR(1) latent dynamics.
 
@@ -150,7 +174,7 @@ class TemporalAMEModel:
             e = eps.view(npairs, 2).double()
             p0 = (l00 * e[:, 0]).float()
             p10 = (l10 * e[:, 0]).float()
-            p1 = (l11 * e[:, 1] + p10.double()).float()
+            p1 = fma_f32(l11 * e[:, 1], p10)
             mu_t = self._mean_seqfma(self.X[:, t, :2], self.X[:, t, 2:])
             dy = mu_t[iu[0], iu[1]] + torch.stack([p0, p1], dim=1)
             self.Y[iu[0], iu[1], t] = dy
@@ -165,12 +189,12 @@ class TemporalAMEModel:
         the reference's fp32 sgemm sums it on the fixture host (MKL: one fused
         multiply-add per k, k ascending; measured bit-exact), but independent of
         the host's BLAS: each step is an exact fp64 product plus the running fp32
-        sum, rounded once to fp32."""
+        sum, rounded once to fp32 (:func:`fma_f32`)."""
         a, b = A[:, 0], A[:, 1]
         U, V = M[:, :self.r].double(), M[:, self.r:].double()
         mult = torch.zeros(A.shape[0], A.shape[0], dtype=torch.float32)
         for k in range(self.r):
-            mult = (torch.outer(U[:, k], V[:, k]) + mult.double()).float()
+            mult = fma_f32(torch.outer(U[:, k], V[:, k]), mult)
         additive = a.unsqueeze(1) + b.unsqueeze(0)
         mu = torch.zeros(A.shape[0], A.shape[0], 2)
         mu[:, :, 0] = additive + mult

@@ -32,7 +32,7 @@ def _free_port():
     return p
 
 
-def _run(n, T, r, method, lr, iters, distributed, depth=None):
+def _run(n, T, r, method, lr, iters, distributed, depth=None, kind=None):
     from ame_amd import TemporalAMEModel, TemporalAMENaiveMFVI, TemporalAMEStructuredMFVI
     m = TemporalAMEModel(n, T, r, seed=21)
     m.generate_data_fast(seed=4)
@@ -45,9 +45,13 @@ def _run(n, T, r, method, lr, iters, distributed, depth=None):
         vi = TemporalAMEStructuredMFVI(m, factorization=method, learning_rate=lr, device=dev,
                                        distributed=distributed, engine_options=opts)
     eng = vi.engine
+    if kind is not None:
+        assert eng.sweep_kind == kind, (eng.sweep_kind, kind)
     if distributed and depth is not None:
         assert eng.pipelined and eng.spec_depth == depth and len(eng.xs) == depth + 1
     h = vi.fit(max_iter=iters, tolerance=0.0, verbose=False)
+    if distributed:   # every peer link passed the setup pre-flight (distributed.py)
+        assert vi._halo.preflight_ok
     return (vi.X_mean.numpy().copy(), vi.X_cov.numpy().copy(),
             [float(e) for e in h["elbo"]], list(h["reconstruction_error"]))
 
@@ -56,25 +60,34 @@ def _worker(rank, world, port, args, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        n, T, r, method, lr, iters, depth = args
-        out = _run(n, T, r, method, lr, iters, True, depth)
+        n, T, r, method, lr, iters, depth, kind = args
+        out = _run(n, T, r, method, lr, iters, True, depth, kind)
         if rank == 0:
             q.put(out)
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n,T,r,method,lr,iters,depth", [
-    (2, 64, 8, 4, "good", 0.5, 3, None), (2, 40, 6, 3, "bad", 1.0, 3, None),
-    (2, 48, 5, 2, "naive", 0.3, 3, None), (3, 50, 9, 3, "good", 0.5, 6, None),
-    (4, 40, 12, 4, "good", 0.7, 6, None),
+V3, W22 = 3, 22   # _lib.AME_SWEEP_V3, _lib.AME_SWEEP_V2_WORKERS
+
+
+@pytest.mark.parametrize("world,n,T,r,method,lr,iters,depth,kind", [
+    (2, 64, 8, 4, "good", 0.5, 3, None, V3), (2, 40, 6, 3, "bad", 1.0, 3, None, V3),
+    (2, 48, 5, 2, "naive", 0.3, 3, None, V3), (3, 50, 9, 3, "good", 0.5, 6, None, V3),
+    (4, 40, 12, 4, "good", 0.7, 6, None, V3),
     # the queue depth the model gives at N = 8: 3 sweeps ahead
     # on 3 and 4 ranks, 8 iterations (several wraps of the state ring)
-    (3, 60, 12, 4, "good", 0.5, 8, 3), (4, 64, 16, 3, "bad", 0.8, 8, 3)])
-def test_ranks_one_gpu(world, n, T, r, method, lr, iters, depth):
+    (3, 60, 12, 4, "good", 0.5, 8, 3, V3), (4, 64, 16, 3, "bad", 0.8, 8, 3, V3),
+    # config 5's sweep kernel (r = 32, d = 66: v2 + seven GEMV-worker workgroups
+    # per slice) time-sharded: the left-halo poll of a rank's first slice beside
+    # the workers' partial ring, 2 and 3 ranks, good / bad / naive, in-order
+    # sweeps over several iterations (kind 22 does not pipeline)
+    (2, 300, 8, 32, "good", 0.5, 3, None, W22), (3, 240, 12, 32, "bad", 0.7, 3, None, W22),
+    (2, 200, 6, 32, "naive", 0.4, 4, None, W22), (3, 301, 9, 32, "good", 0.01, 3, None, W22)])
+def test_ranks_one_gpu(world, n, T, r, method, lr, iters, depth, kind):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    args = (n, T, r, method, lr, iters, depth)
+    args = (n, T, r, method, lr, iters, depth, kind)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -94,9 +107,67 @@ def test_ranks_one_gpu(world, n, T, r, method, lr, iters, depth):
             p.join()
     assert codes == [0] * world, f"rank exit codes {codes}"
     mean_d, cov_d, elbo_d, rec_d = result
-    n, T, r, method, lr, iters, _ = args
-    mean_s, cov_s, elbo_s, rec_s = _run(n, T, r, method, lr, iters, False)
+    n, T, r, method, lr, iters, _, kind = args
+    mean_s, cov_s, elbo_s, rec_s = _run(n, T, r, method, lr, iters, False, kind=kind)
     assert np.array_equal(mean_d, mean_s)
     assert np.array_equal(cov_d, cov_s)
     assert np.allclose(elbo_d, elbo_s, rtol=1e-6, atol=0)
     assert np.allclose(rec_d, rec_s, rtol=1e-12, atol=0)
+
+
+def _preflight_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ame_amd import TemporalAMEModel, TemporalAMEStructuredMFVI
+        m = TemporalAMEModel(40, 6, 2, seed=3)
+        m.generate_data_fast(seed=3)
+        vi = TemporalAMEStructuredMFVI(m, learning_rate=0.5, device=torch.device("cuda", 0),
+                                       distributed=True)
+        vi.fit(max_iter=1, tolerance=0.0, verbose=False)
+        halo = vi._halo
+        assert halo.preflight_ok
+        # a link that delivers the wrong word: rank 0 stores a sentinel addressed
+        # to another owner into rank 1's halo; rank 1 must name the pair, rank 0
+        # must learn of it from the all_reduce, and neither may hang
+        if rank == 0:
+            real = halo._sentinel
+            halo._sentinel = lambda kind, writer, owner: real(kind, writer, owner + 7)
+        msg = None
+        try:
+            halo._preflight(vi.engine)
+        except RuntimeError as e:
+            msg = str(e)
+        # the buffers were zeroed after the check: the sweep still runs
+        vi.fit(max_iter=1, tolerance=0.0, verbose=False)
+        q.put((rank, msg))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_preflight_detects_bad_link():
+    """The setup pre-flight of the peer links (distributed.py _preflight) raises
+    on both ranks, naming the failing pair on its owner, when the word that
+    arrives is not the sentinel that was sent."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_preflight_worker, args=(rk, 2, port, q)) for rk in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(2):
+            rank, msg = q.get(timeout=150)
+            got[rank] = msg
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.exitcode is None:
+                p.kill()
+                p.join()
+    assert [p.exitcode for p in procs] == [0, 0]
+    assert got[1] is not None and "rank 0 -> rank 1 (left halo)" in got[1], got[1]
+    assert got[0] is not None and "another rank" in got[0], got[0]

@@ -1,7 +1,8 @@
 #!/bin/bash
 # SQ / SQC counters of the sweep kernel (one --pmc pass per counter group);
-# extra arguments go to bench.py (e.g. --n 4096 --t-per-gpu 32 --latent-dim 32).
-# usage: tools/gpu_pmc_sweep.sh TAG [bench args...]
+# extra arguments go to bench.py (e.g. --n 4096 --t-per-gpu 32 --latent-dim 32);
+# N / TL (env, default 1024 / 128) normalise the counters per workgroup-step.
+# usage: [N=4096 TL=32] tools/gpu_pmc_sweep.sh TAG [bench args...]
 set -o pipefail
 OUT=gpurun_out/${1:-pmcsq}; shift; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
@@ -14,4 +15,4 @@ for P in A B C; do
     -d $OUT/p$P -o pmc -- python3 -u bench.py --no-cpu-baseline --steps 3 --warmup 1 "$@" \
     > $OUT/p$P.log 2>&1 || { echo "pmc $P failed"; tail -5 $OUT/p$P.log; exit 1; }
 done
-python3 tools/pmc_sq.py $OUT 1024 128 | tee $OUT/sq.txt
+python3 tools/pmc_sq.py $OUT ${N:-1024} ${TL:-128} | tee $OUT/sq.txt

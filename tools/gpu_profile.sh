@@ -21,6 +21,8 @@ cat $OUT/pmc_pairs.json
 python3 tools/pmc_summary.py $OUT n1024_T128_r16_good 1024 128 16 > $OUT/pmc_latest.json || exit 1
 cp $OUT/pmc_latest.json profiles/pmc_latest.json
 cat $OUT/pmc_latest.json
+# SQ counters of the sweep (in-order sweeps: no pipelined launch waits in the counts)
+bash tools/gpu_pmc_sweep.sh $TAG/sq --no-pipeline || exit 1
 timeout -k 10 400 python3 -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -20 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- \

@@ -1,7 +1,7 @@
 """Does the ELBO side (covariance-terms + ELBO kernels, run beside the pipelined
 sweeps) slow the sweep down?  Config 3 by default, one GPU:
 
-    python tools/interference.py --build TAG DEF1,DEF2   # here: variant library _build/libame_amd_var{TAG}.so
+    python tools/interference.py --build TAG DEF1,DEF2   # here: variant library tools/_lib/libame_amd_var{TAG}.so
     python tools/interference.py [--shape n,T,r] [TAG ...]   # GPU box: per library, fit vs sweeps-only
 
 (A) ms per fit() iteration (the bench's loop); (B) ms per sweep when the same
@@ -15,7 +15,8 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "python-temporal-ame-svi_amd")
-BDIR = os.path.join(PKG, "ame_amd", "_build")
+BDIR = os.path.join(PKG, "ame_amd", "_build")      # objects (not shipped to the GPU box)
+LIBDIR = os.path.join(ROOT, "tools", "_lib")         # variant libraries (shipped)
 
 def _unsplit_sources():
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
@@ -27,6 +28,7 @@ def _unsplit_sources():
 
 def build(tag, defs):
     os.makedirs(BDIR, exist_ok=True)
+    os.makedirs(LIBDIR, exist_ok=True)
     csrc = os.path.join(PKG, "ame_amd", "csrc")
     objs = []
     procs = []
@@ -38,7 +40,7 @@ def build(tag, defs):
         objs.append(o)
     for p in procs:
         assert p.wait() == 0
-    so = os.path.join(BDIR, f"libame_amd_var{tag}.so")
+    so = os.path.join(LIBDIR, f"libame_amd_var{tag}.so")
     subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", so, *objs])
     print("built", so)
 
@@ -97,7 +99,7 @@ if __name__ == "__main__":
         for tag in ["default"] + args:
             env = dict(os.environ)
             if tag != "default":
-                env["AME_LIB_PATH"] = os.path.join(BDIR, f"libame_amd_var{tag}.so")
+                env["AME_LIB_PATH"] = os.path.join(LIBDIR, f"libame_amd_var{tag}.so")
             for rep in range(2):
                 r = subprocess.run([sys.executable, "-u", __file__, "--child", shape], env=env, capture_output=True,
                                    text=True, timeout=300)

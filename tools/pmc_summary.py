@@ -58,6 +58,15 @@ def main():
                         "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
                         "hbm_bytes_per_launch": rd + wr, "alg_bytes": alg[cls],
                         "traffic_over_alg": (rd + wr) / alg[cls]}
+    pp = os.path.join(outdir, "pmc_pairs.json")   # MFMA pass (tools/pmc_pairs.py), if taken
+    if "pairs" in kernels and os.path.exists(pp):
+        z = json.load(open(pp))
+        if z.get("mfma_busy_est") is not None:
+            kernels["pairs"]["mfma_busy"] = z["mfma_busy_est"]
+            kernels["pairs"]["mfma_counters"] = {k: z.get(k) for k in
+                                                 ("SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE")}
+            kernels["pairs"]["mfma_method"] = ("SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs "
+                                               "x 256 CUs x 4 SIMDs), median dispatch")
     out = {"config_tag": tag,
            "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; FETCH_SIZE x2 (gfx950)",
            "kernels": kernels}

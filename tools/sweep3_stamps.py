@@ -1,6 +1,6 @@
 """Diagnostic for the v3 sweep (ame_sweep3.hip): in-kernel s_memtime stamps.
 
-    python tools/sweep3_stamps.py --build      # here: hipcc -DAME_STAMPS -> _build/libame_amd_stamps3.so
+    python tools/sweep3_stamps.py --build      # here: hipcc -DAME_STAMPS -> tools/_lib/libame_amd_stamps3.so
     python tools/sweep3_stamps.py [--tag=T] [--iters=K]   # GPU box: config-3 fit, per-wave timelines
                                                # of the last sweep (K > 2: a pipelined steady-state one)
 
@@ -15,9 +15,10 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "python-temporal-ame-svi_amd")
-BDIR = os.path.join(PKG, "ame_amd", "_build")
+BDIR = os.path.join(PKG, "ame_amd", "_build")      # objects (not shipped to the GPU box)
+LIBDIR = os.path.join(ROOT, "tools", "_lib")         # variant libraries (shipped)
 TAG = ([a.split("=", 1)[1] for a in sys.argv if a.startswith("--tag=")] or [""])[0]
-SO = os.path.join(BDIR, f"libame_amd_stamps3{TAG}.so")
+SO = os.path.join(LIBDIR, f"libame_amd_stamps3{TAG}.so")
 
 def _unsplit_sources():
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
@@ -44,6 +45,7 @@ WAVES = ["solver(w0)"] + [f"hw{w - 1}(w{w})" for w in range(1, 8)]
 
 def build(r=16):
     os.makedirs(BDIR, exist_ok=True)
+    os.makedirs(LIBDIR, exist_ok=True)
     csrc = os.path.join(PKG, "ame_amd", "csrc")
     defs = [f"-D{d}" for d in (" ".join(a for a in sys.argv if a.startswith("--defs=")).replace(
         "--defs=", "")).split(",") if d]

@@ -1,7 +1,7 @@
 """Diagnostic: per-phase cycle shares of one sweep step (in-kernel s_memtime stamps).
 
-    python tools/sweep_stamps.py --build [--r=16]          # here: hipcc -DAME_STAMPS -> _build/libame_amd_stamps.so
-    python tools/sweep_stamps.py [--n=1024 --T=128 --r=16 --variant=good] # GPU box: v2 sweep (AME_SWEEP_V2=1), phase shares
+    python tools/sweep_stamps.py --build [--r=16]          # here: hipcc -DAME_STAMPS -> tools/_lib/libame_amd_stamps.so
+    python tools/sweep_stamps.py [--n=1024 --T=128 --r=16 --variant=good --kind=20] # GPU box: v2 sweep, phase shares
 
 Stamps are taken by thread 0 of the middle lane for 16 nodes in steady state.
 The stamped build's run time is never quoted; only its SHARES are meaningful.
@@ -13,8 +13,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "python-temporal-ame-svi_amd")
-BDIR = os.path.join(PKG, "ame_amd", "_build")
-SO = os.path.join(BDIR, "libame_amd_stamps.so")
+BDIR = os.path.join(PKG, "ame_amd", "_build")      # objects (not shipped to the GPU box)
+LIBDIR = os.path.join(ROOT, "tools", "_lib")         # variant libraries (shipped)
+SO = os.path.join(LIBDIR, "libame_amd_stamps.so")
 PHASES = ["phase 1: K-matvecs + z staging", "phase 2: wave0 Woodbury | waves1-3 GEMV+poll",
           "phase 3: K rank-4 update + cov write + AR", "loop (+ cov prefetch issue)"]
 
@@ -36,6 +37,7 @@ def _opt(name, default=None):
 def build(r=16):
     """--defs=A,B adds -DA -DB (ablation switches); --tag=X names the library."""
     os.makedirs(BDIR, exist_ok=True)
+    os.makedirs(LIBDIR, exist_ok=True)
     csrc = os.path.join(PKG, "ame_amd", "csrc")
     defs = [f"-D{d}" for d in (_opt("--defs") or "").split(",") if d]
     tag = _opt("--tag", "")
@@ -53,7 +55,6 @@ def build(r=16):
 
 def run():
     os.environ["AME_LIB_PATH"] = SO.replace(".so", f"{_opt('--tag', '')}.so")
-    os.environ["AME_SWEEP_V2"] = "1"
     n, T, r = int(_opt("--n", 1024)), int(_opt("--T", 128)), int(_opt("--r", 16))
     sys.path.insert(0, PKG)
     import torch
@@ -63,10 +64,17 @@ def run():
     m = TemporalAMEModel(n, T, r, seed=42)
     m.generate_data_fast(device=dev)
     variant = _opt("--variant", "good")
+    # the stamps live in the v2 kernel: request a v2 kind explicitly (AUTO would
+    # pick v3 at n=1024, r=16, whose stamp buffer this tool does not read)
+    kind = int(_opt("--kind", _lib.AME_SWEEP_V2_AUTO))
+    opts = {"sweep_kernel": kind}
     if variant == "naive":
-        vi = TemporalAMENaiveMFVI(m, learning_rate=0.01, device=dev)
+        vi = TemporalAMENaiveMFVI(m, learning_rate=0.01, device=dev, engine_options=opts)
     else:
-        vi = TemporalAMEStructuredMFVI(m, factorization=variant, learning_rate=0.01, device=dev)
+        vi = TemporalAMEStructuredMFVI(m, factorization=variant, learning_rate=0.01, device=dev,
+                                       engine_options=opts)
+    assert vi.engine.sweep_kind in (_lib.AME_SWEEP_V2_LDS, _lib.AME_SWEEP_V2_HBM,
+                                    _lib.AME_SWEEP_V2_WORKERS), vi.engine.sweep_kind
     vi.fit(max_iter=2, tolerance=0.0, verbose=False)
     torch.cuda.synchronize()
     L = _lib.lib()

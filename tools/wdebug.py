@@ -3,8 +3,9 @@
 import os, subprocess, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "python-temporal-ame-svi_amd")
-BDIR = os.path.join(PKG, "ame_amd", "_build")
-SO = os.path.join(BDIR, "libame_amd_wdbg.so")
+BDIR = os.path.join(PKG, "ame_amd", "_build")      # objects (not shipped to the GPU box)
+LIBDIR = os.path.join(ROOT, "tools", "_lib")         # variant libraries (shipped)
+SO = os.path.join(LIBDIR, "libame_amd_wdbg.so")
 
 def _unsplit_sources():
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
@@ -13,6 +14,8 @@ def _unsplit_sources():
     return UNSPLIT_SOURCES
 
 if "--build" in sys.argv:
+    os.makedirs(BDIR, exist_ok=True)
+    os.makedirs(LIBDIR, exist_ok=True)
     objs = []
     for src in _unsplit_sources():
         o = os.path.join(BDIR, src.replace(".hip", "_wd.o"))
