@@ -318,7 +318,9 @@ def test_config5_rank_shape(method, gpu_device):
     _check_prefix(got_m[:K], got_c[:K], rm, rc, rm32)
     KF = n if method == "good" else 600
     Xm, Xc = x1.astype(np.float64), c1[:KF].astype(np.float64)
-    O.sweep_stats(Y32, Xm, Xc, _params(m), method, lr, nodes=range(KF))
+    for a in range(0, KF, 1024):   # chunks, with a progress line (about 25 s each)
+        O.sweep_stats(Y32, Xm, Xc, _params(m), method, lr, nodes=range(a, min(KF, a + 1024)))
+        print(f"config 5 {method}: oracle replay at node {min(KF, a + 1024)} of {KF}", flush=True)
     err = np.abs(got_m[:KF].astype(np.float64) - Xm[:KF]).max()
     cerr = np.abs(got_c[:KF].astype(np.float64) - Xc).max()
     print(f"config 5 {method}: nodes 0..{KF - 1} vs fp64 oracle: max|dmean| {err:.3e} "
