@@ -132,7 +132,8 @@ def _preflight_worker(rank, world, port, q):
         # must learn of it from the all_reduce, and neither may hang
         if rank == 0:
             real = halo._sentinel
-            halo._sentinel = lambda kind, writer, owner: real(kind, writer, owner + 7)
+            halo._sentinel = lambda kind, writer, owner: real(kind, writer,
+                                                              owner + 7 if kind == 1 else owner)
         msg = None
         try:
             halo._preflight(vi.engine)
