@@ -39,7 +39,8 @@ for _w in range(1, 8):
                  "GEMV",
                  "DMA" if _hw == 6 else ("spin" if _hw <= 2 else "-"),
                  "gemv-fma", "gemv-rs",
-                 "vmwait" if _hw == 6 else "end"]
+                 "vmwait" if _hw == 6 else "end",
+                 "pre-pring"]
 WAVES = ["solver(w0)"] + [f"hw{w - 1}(w{w})" for w in range(1, 8)]
 
 
