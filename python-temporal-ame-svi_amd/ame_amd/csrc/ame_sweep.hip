@@ -867,6 +867,10 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     gemv_reduce(0);
     ar_terms(0);
     __syncthreads();
+    // WK: the natural parameter's two parts (h_obs, AR terms) summed once into
+    // gob(node)[k] (the K-matvec items of phase 1 read one value instead of two)
+    if (WK && tid < D) gob(0)[tid] += gob(0)[D + tid];
+    if constexpr (WK) __syncthreads();
 
     float y_prev0 = 0.f, y_prev1 = 0.f;   // y_{i,i-1} (raw)
     for (int i = 0; i < n; ++i) {
@@ -913,8 +917,20 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 const float* vv = row0 ? (src + R) : src;
                 const double* kr = K + k * KS + cb;
                 double p4[4] = {K[k * KS + (row0 ? 0 : 1)], 0.0, 0.0, 0.0};
+                if constexpr (R % 2 == 0) {
+                    // the node vector as 8-byte pairs (it starts 8-byte aligned when
+                    // r is even): half the LDS read instructions, same sums
+                    const float2* v2 = (const float2*)vv;
 #pragma unroll
-                for (int c = 0; c < R; ++c) p4[c & 3] = fma(kr[c], (double)vv[c], p4[c & 3]);
+                    for (int c2 = 0; c2 < R / 2; ++c2) {
+                        const float2 t = v2[c2];
+                        p4[(2 * c2) & 3] = fma(kr[2 * c2], (double)t.x, p4[(2 * c2) & 3]);
+                        p4[(2 * c2 + 1) & 3] = fma(kr[2 * c2 + 1], (double)t.y, p4[(2 * c2 + 1) & 3]);
+                    }
+                } else {
+#pragma unroll
+                    for (int c = 0; c < R; ++c) p4[c & 3] = fma(kr[c], (double)vv[c], p4[c & 3]);
+                }
                 return (p4[0] + p4[1]) + (p4[2] + p4[3]);
             };
             auto chunk = [&](int r2) -> double {   // u, (U,V)-part chunk r2 = ch * D + k
@@ -925,12 +941,13 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
 #pragma unroll
                 for (int mm = 0; mm < 16; ++mm) {
                     const int m = m0 + mm;
-                    if (m < D) p2[mm & 1] = fma(K[k * KS + m], gi[m] + gi[D + m], p2[mm & 1]);
+                    if (m < D) p2[mm & 1] = fma(K[k * KS + m], WK ? gi[m] : gi[m] + gi[D + m], p2[mm & 1]);
                 }
                 return p2[0] + p2[1];
             };
             auto apart = [&](int k) -> double {   // u, a-part
                 const double* gi = gob(i);
+                if constexpr (WK) return K[k * KS + 0] * gi[0] + K[k * KS + 1] * gi[1];
                 return K[k * KS + 0] * (gi[0] + gi[D]) + K[k * KS + 1] * (gi[1] + gi[D + 1]);
             };
             if constexpr (R == 32 && AME_NT == 256) {
@@ -976,7 +993,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
 #pragma unroll
                     for (int mm = 0; mm < 2; ++mm) {
                         const int m = m0 + mm;
-                        if (m < D) v = fma(K[k * KS + m], gi[m] + gi[D + m], v);
+                        if (m < D) v = fma(K[k * KS + m], WK ? gi[m] : gi[m] + gi[D + m], v);
                     }
                     v += __shfl_xor(v, 1);
                     v += __shfl_xor(v, 2);
@@ -1034,7 +1051,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                     ua[h] = vec[4 * D + k];
 #pragma unroll
                     for (int ch = 0; ch < US; ++ch) uM[h] += vec[(5 + ch) * D + k];
-                    gk[h] = gob(i)[k] + gob(i)[D + k];
+                    gk[h] = WK ? gob(i)[k] : gob(i)[k] + gob(i)[D + k];
                     K0[h] = K[k * KS + 0];
                     K1[h] = K[k * KS + 1];
                     if (k == 0) { jp0[h] = 1.0; jn0[h] = 1.0; }
@@ -1234,6 +1251,9 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         lds_barrier();   // B2
         STAMP(2);
         // ---------------- phase 3 ----------------
+        // WK: node i+1's natural parameter in one piece (its parts were written
+        // in phase 2, before B2; read from phase 1 of the next step on)
+        if (WK && has_next && tid < D) gob(i + 1)[tid] += gob(i + 1)[D + tid];
         {
             // the LDS reads of QB rounds first, then their stores: a round's K / cst
             // stores otherwise keep the next round's reads behind them (the compiler

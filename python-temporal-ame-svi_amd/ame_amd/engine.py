@@ -103,9 +103,11 @@ class EngineOptions:
 # wavefront's fill over all T_total slices plus one chain plus the ELBO kernels
 # and the all_reduce; by then sweep k + 1 + depth must already be queued:
 #     (1 + depth) P >= fill + C + delta,   fill = F (T_total - 1) steps.
-# F = 2.6 node steps of lag per slice (lane start offset 6.6 us at 2.6 us per
-# step, profiles/r01_s3_sweep3_stamps.txt); delta ~ 128 steps (0.33 ms).
-FILL_STEPS_PER_SLICE = 2.6
+# F = node steps of lag per slice: 2.94 measured in round 4 (lane start offset
+# 890 us over 127 slices at 2.38 us per step, profiles/r04_v3_stamps_head.txt;
+# 2.6 in round 1), rounded up to 3.0 -- a deeper queue only costs a state slot;
+# delta ~ 128 steps (0.33 ms).
+FILL_STEPS_PER_SLICE = 3.0
 ELBO_READ_STEPS = 128
 MAX_SPEC_DEPTH = 8
 

@@ -20,13 +20,13 @@ def test_queue_depth_model():
     assert derive_spec_depth(1024, 128) == 2
     assert derive_spec_depth(1024, 256) == 2
     assert derive_spec_depth(1024, 512) == 2
-    assert derive_spec_depth(1024, 1024) == 3      # N = 8: fill 2.6 x 1023 steps > 2 chains
-    # the model's margin at N = 8 and depth 3: (1 + 3) n >= 2.6 (T - 1) + n + 128
+    assert derive_spec_depth(1024, 1024) == 4      # N = 8: fill 3.0 x 1023 steps > 3 chains
+    # the model's margin at N = 8 and depth 4: (1 + 4) n >= 3.0 (T - 1) + n + 128
     n, T = 1024, 1024
-    assert (1 + 3) * n >= 2.6 * (T - 1) + n + 128
-    assert (1 + 2) * n < 2.6 * (T - 1) + n + 128   # depth 2 would stall
+    assert (1 + 4) * n >= 3.0 * (T - 1) + n + 128
+    assert (1 + 3) * n < 3.0 * (T - 1) + n + 128   # depth 3 would stall (by ~1 %)
     # short chains, many slices: deeper, capped
-    assert derive_spec_depth(256, 512) == 6
+    assert derive_spec_depth(256, 512) == 7
     assert derive_spec_depth(16, 4096) == 8
     assert derive_spec_depth(4096, 32) == 2
 

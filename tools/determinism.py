@@ -2,6 +2,10 @@
 fits from the same seed must give bit-equal means, single-process and split
 over two ranks on one GPU (peer-buffer halo).  Prints the first
 (iteration, node, slice) that differs.   GPU box:  python tools/determinism.py [reps]
+
+Other cases through the environment: DET_SHAPE=n,T,r  DET_VARIANT=good|bad|naive
+DET_WORLD=ranks  DET_LR  DET_ITERS  DET_DEPTH (queue depth)  DET_SEEDS=model,data
+(e.g. the tests/test_gpu_distributed.py case 4 ranks, 64,16,3, bad, 0.8, 8, 3, 21,4).
 """
 import os
 import socket
@@ -11,17 +15,31 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "python-temporal-ame-svi_amd"))
-ITERS = 3
+ITERS = int(os.environ.get("DET_ITERS", "3"))
+SHAPE = tuple(int(x) for x in os.environ.get("DET_SHAPE", "1024,128,16").split(","))
+VARIANT = os.environ.get("DET_VARIANT", "good")
+WORLD = int(os.environ.get("DET_WORLD", "2"))
+LR = float(os.environ.get("DET_LR", "0.01"))
+DEPTH = os.environ.get("DET_DEPTH")
+SEEDS = tuple(int(x) for x in os.environ.get("DET_SEEDS", "42,-1").split(","))
 
 
 def run(distributed):
     import torch
-    from ame_amd import TemporalAMEModel, TemporalAMEStructuredMFVI
+    from ame_amd import TemporalAMEModel, TemporalAMENaiveMFVI, TemporalAMEStructuredMFVI
     dev = torch.device("cuda", 0)
-    m = TemporalAMEModel(1024, 128, 16, seed=42)
-    m.generate_data_fast(device=dev)
-    vi = TemporalAMEStructuredMFVI(m, factorization="good", learning_rate=0.01, device=dev,
-                                   distributed=distributed)
+    m = TemporalAMEModel(*SHAPE, seed=SEEDS[0])
+    if SEEDS[1] >= 0:
+        m.generate_data_fast(seed=SEEDS[1])
+    else:
+        m.generate_data_fast(device=dev)
+    opts = {} if DEPTH is None else {"spec_depth": int(DEPTH)}
+    if VARIANT == "naive":
+        vi = TemporalAMENaiveMFVI(m, learning_rate=LR, device=dev, distributed=distributed,
+                                  engine_options=opts)
+    else:
+        vi = TemporalAMEStructuredMFVI(m, factorization=VARIANT, learning_rate=LR, device=dev,
+                                       distributed=distributed, engine_options=opts)
     out = []
     if os.environ.get("DET_PIPELINED", "1") == "1":   # one fit: pipelined sweeps
         vi.fit(max_iter=ITERS, tolerance=0.0, verbose=False)
@@ -52,7 +70,7 @@ def run_dist():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    procs = [ctx.Process(target=worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=worker, args=(r, WORLD, port, q)) for r in range(WORLD)]
     for p in procs:
         p.start()
     out = q.get(timeout=150)
@@ -78,7 +96,7 @@ def main():
     bad = 0
     for r in range(reps):
         ok = compare(f"single rep {r}", ref, run(None))
-        ok &= compare(f"2-rank rep {r}", ref, run_dist())
+        ok &= compare(f"{WORLD}-rank rep {r}", ref, run_dist())
         print(f"rep {r}: {'equal' if ok else 'DIFFERENT'}", flush=True)
         bad += not ok
     print("DETERMINISTIC" if bad == 0 else f"NONDETERMINISTIC in {bad}/{reps} reps")

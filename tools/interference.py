@@ -1,7 +1,7 @@
 """Does the ELBO side (covariance-terms + ELBO kernels, run beside the pipelined
 sweeps) slow the sweep down?  Config 3 by default, one GPU:
 
-    python tools/interference.py --build TAG DEF1,DEF2   # here: variant library tools/_lib/libame_amd_var{TAG}.so
+    [AME_VAR_R=32] python tools/interference.py --build TAG DEF1,DEF2   # here: variant library tools/_lib/libame_amd_var{TAG}.so (r = 16 unless AME_VAR_R)
     python tools/interference.py [--shape n,T,r] [TAG ...]   # GPU box: per library, fit vs sweeps-only
 
 (A) ms per fit() iteration (the bench's loop); (B) ms per sweep when the same
@@ -35,7 +35,8 @@ def build(tag, defs):
     for src in _unsplit_sources():
         o = os.path.join(BDIR, src.replace(".hip", f"_var{tag}.o"))
         procs.append(subprocess.Popen(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17",
-                                       "-DAME_ONLY_R=16", *[f"-D{d}" for d in defs if d], "-Wno-pass-failed",
+                                       f"-DAME_ONLY_R={os.environ.get('AME_VAR_R', '16')}",
+                                       *[f"-D{d}" for d in defs if d], "-Wno-pass-failed",
                                        "-c", os.path.join(csrc, src), "-o", o]))
         objs.append(o)
     for p in procs:
