@@ -114,7 +114,8 @@ typedef struct ame_sweep_args {
     uint32_t* status;            /* [1] error word */
     double* work;                /* scratch, >= ame_sweep_work_size() doubles: 0 for the v3
                                     sweep; the GEMV workers' partial ring (zeroed by the call
-                                    itself) for v2 with workers (kind 22: n = 4096, r = 32, ...);
+                                    itself) and the right-neighbour AR terms (filled by the call)
+                                    for v2 with workers (kind 22: n = 4096, r = 32, ...);
                                     [T_local][n][2r] fp32 (U,V) copy when v2 keeps the slice in
                                     HBM without workers (kind 21); may be NULL
                                     when the size is 0 */

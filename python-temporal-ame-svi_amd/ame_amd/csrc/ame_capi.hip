@@ -279,7 +279,8 @@ long long ame_sweep_work_size(const ame_dims* dims, int kind) {
         case AME_SWEEP_V2_LDS: return 0;
         // [T_local][n][2r] fp32 (U,V) copy
         case AME_SWEEP_V2_HBM: return ((long long)dims->T_local * dims->n * 2 * dims->r + 1) / 2;
-        case AME_SWEEP_V2_WORKERS: return ame_v2_ring_doubles(dims);
+        // partial ring, then the precomputed right AR terms
+        case AME_SWEEP_V2_WORKERS: return ame_v2_ring_doubles(dims) + ame_v2_arr_doubles(dims);
         default: return fail("ame_sweep_work_size: %d is not a concrete sweep kind", kind);
     }
 }

@@ -42,6 +42,22 @@ __device__ __forceinline__ void gran_store_system(uint64_t* p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// a*b + c*d with both products and the sum rounded, never contracted into an
+// FMA: the reference's fp32 elementwise forms (damping lr * new + (1 - lr) * old,
+// z = R^-1 y).  __fadd_rn / __fmul_rn are plain + and * in this HIP, which
+// -ffp-contract=fast may fuse -- differently for a covariance entry and its
+// mirror, so the damped covariance was not exactly symmetric.
+#ifdef AME_EXP_FUSE
+__device__ __forceinline__ float mul_add_rn(float a, float b, float c, float d) {
+    return a * b + c * d;
+}
+#else
+__device__ __forceinline__ float mul_add_rn(float a, float b, float c, float d) {
+#pragma clang fp contract(off)
+    return a * b + c * d;
+}
+#endif
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -132,6 +148,12 @@ __host__ __device__ inline long long ame_v2_mode_lds(int n, int R, int mode) {
 }
 __host__ __device__ inline long long ame_v2_ring_doubles(const ame_dims* d) {
     return (long long)d->T_local * AME_GW * AME_GW_RING * (2 * d->r + 2);
+}
+// MODE 2: the precomputed right-neighbour AR terms, [T_local][n][NPA * d] past the
+// ring (NPA = AR row parts on 192 threads: ArPart<R, true> in ame_sweep.hip)
+__host__ __device__ inline long long ame_v2_arr_doubles(const ame_dims* d) {
+    const int D = 2 + 2 * d->r, npa = (4 * D <= 192) ? 4 : 2;
+    return (long long)d->T_local * d->n * npa * D;
 }
 
 

@@ -47,7 +47,7 @@
 // T_local/2 records s_memtime after each phase for nodes
 // [AME_STAMP_I0, AME_STAMP_I0 + 16).  Never compiled into the product library.
 #define AME_STAMP_I0 256
-#define AME_STAMP_NPH 16
+#define AME_STAMP_NPH 32
 __device__ unsigned long long g_ame_stamps[16 * AME_STAMP_NPH];
 #define STAMP(ph) STAMPW(ph, 0)
 #define STAMPW(ph, who)                                                                    \
@@ -172,6 +172,55 @@ __device__ __forceinline__ void tri_decode(int e, int& k, int& m) {
     m = e - k * (k + 1) / 2;
 }
 
+// AR-term partition of the natural parameter (the sweep's AR threads): thread
+// `at` < NPA * D owns row k = at / NPA, part pp = at % NPA, columns
+// [pp * MC, pp * MC + MC).  WK runs the AR terms on 192 threads, the others on
+// the whole workgroup.
+template <int R, bool WK>
+struct ArPart {
+    static constexpr int D = 2 + 2 * R;
+    static constexpr int ART = WK ? 192 : AME_NT;
+    static constexpr int NPA = (4 * D <= ART) ? 4 : 2;
+    static constexpr int MC = (D + NPA - 1) / NPA;
+};
+
+// MODE 2 (GEMV workers): the right-neighbour AR term PhiTQi mu_{j,t+1}^old of
+// every node j, per AR thread part, before the sweep.  Its inputs are old means
+// (fixed for the whole sweep), so the sweep reads one value per thread and
+// step instead of forming it on its critical path.  Same products, order and
+// zero padding as the in-sweep form (ar_terms), so the sums are unchanged.
+// One workgroup per (slice, node); out[(tl * n + j) * NPA * D + at].
+template <int R>
+__global__ void __launch_bounds__(AME_NT)
+ame_ar_right_kernel(ame_dims dm, ame_sweep_args a, double* out) {
+    using P = ArPart<R, true>;
+    constexpr int D = P::D, NPA = P::NPA, MC = P::MC;
+    const int n = dm.n, TL = dm.T_local, Tt = dm.T_total;
+    const int tl = (int)blockIdx.x / n, j = (int)blockIdx.x - tl * n;
+    const int tg = dm.t_begin + tl;
+    __shared__ float mr_s[D];
+    const int at = threadIdx.x;
+    if (at < D) {
+        float v = 0.f;
+        if (tg < Tt - 1)
+            v = (tl < TL - 1) ? a.x_old[((size_t)(tl + 1) * n + j) * D + at] : a.next_old[(size_t)j * D + at];
+        mr_s[at] = v;
+    }
+    __syncthreads();
+    if (at >= NPA * D) return;
+    const int k = at / NPA, pp = at % NPA;
+    const size_t DD = (size_t)D * D;
+    double pR[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int mm = 0; mm < MC; ++mm) {
+        const int m = pp * MC + mm;
+        const double c = (m < D) ? a.consts[4 * DD + (size_t)k * D + m] : 0.0;
+        const float x = (m < D) ? mr_s[m] : 0.f;
+        pR[mm & 3] = fma(c, (double)x, pR[mm & 3]);
+    }
+    out[((size_t)tl * n + j) * (NPA * D) + at] = (pR[0] + pR[1]) + (pR[2] + pR[3]);
+}
+
 // GEMV worker (MODE 2): workgroup TL + t*AME_GW + g owns nodes
 // [g*NW, (g+1)*NW) of slice t, NW = ceil(n / AME_GW); wave q holds nodes
 // base + q + 4s (s < AME_GW_MAXPW), lane c column c of (U,V), in registers.
@@ -277,7 +326,10 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
             }
         }
         if (m + 1 < n) y_prefetch(m + 1);
-        __syncthreads();
+        // LDS-only barriers in this loop: __syncthreads() would also wait for the
+        // Y prefetch just issued and for the last partial's store (vmcnt(0)),
+        // a full memory round trip per node
+        lds_barrier();
         WSTAMP(2);
         // U_c -> h_V (z1), V -> h_U (z0); four independent chains
         float a4[4] = {0.f, 0.f, 0.f, 0.f};
@@ -310,7 +362,7 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
             red[q * PW + M2] = s0;
             red[q * PW + M2 + 1] = s1;
         }
-        __syncthreads();
+        lds_barrier();
         if (tid < PW) {
             const float v = ((red[tid] + red[PW + tid]) + red[2 * PW + tid]) + red[3 * PW + tid];
             const uint32_t tag = ame_gw_tag(a.epoch, m);
@@ -339,9 +391,9 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     constexpr int VEC = (R % 4 == 0) ? 4 : ((R % 2 == 0) ? 2 : 1);
     constexpr int CW = M2 / VEC, GW = 192 / CW, PW = M2 + 2;
     // AR row parts; WK: the AR terms run on waves 1-3 (192 threads) in phase 2
-    constexpr int ART = WK ? 192 : AME_NT;
-    constexpr int NPA = (4 * D <= ART) ? 4 : 2;
-    constexpr int MC = (D + NPA - 1) / NPA;
+    constexpr int ART = ArPart<R, WK>::ART;
+    constexpr int NPA = ArPart<R, WK>::NPA;
+    constexpr int MC = ArPart<R, WK>::MC;
     static_assert(D <= 128 && 128 + D <= AME_NT && NPA * D <= ART, "sweep v2: D too large");
     constexpr int NLT = D * (D + 1) / 2, LTQ = (NLT + AME_NT - 1) / AME_NT;
     const int n = dm.n, TL = dm.T_local, Tt = dm.T_total;
@@ -486,7 +538,9 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     }
 
     const int at = WK ? tid - 64 : tid;   // AR thread index
-    double qiphi[MC], phitqi[MC];   // AR rows: thread (k = at / NPA, part = at % NPA)
+    // AR rows: thread (k = at / NPA, part = at % NPA); WK reads the PhiTQi half
+    // precomputed (ame_ar_right_kernel)
+    double qiphi[MC], phitqi[WK ? 1 : MC];
     {
         const int k = at / NPA, pp = at % NPA;
 #pragma unroll
@@ -494,7 +548,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             const int m = pp * MC + mm;
             const bool ok = (at >= 0) && (at < NPA * D) && (m < D);
             qiphi[mm] = ok ? a.consts[3 * DD + (size_t)k * D + m] : 0.0;
-            phitqi[mm] = ok ? a.consts[4 * DD + (size_t)k * D + m] : 0.0;
+            if constexpr (!WK) phitqi[mm] = ok ? a.consts[4 * DD + (size_t)k * D + m] : 0.0;
         }
     }
     int lk[LTQ], lm[LTQ];   // lower-triangle entries owned for the update / cov write
@@ -505,6 +559,15 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         if (e < NLT) tri_decode(e, k, m);
         lk[qq] = k;
         lm[qq] = m;
+    }
+    // per-entry flags as bits of one register (bit qq): diagonal entry, and an
+    // entry off the block diagonal of the bad factorization.  As lane masks the
+    // compiler kept them in SGPR pairs, which spill (v_readlane per use)
+    uint32_t dflag = 0u, oflag = 0u;
+#pragma unroll
+    for (int qq = 0; qq < LTQ; ++qq) {
+        if (lk[qq] >= 0 && lk[qq] == lm[qq]) dflag |= 1u << qq;
+        if (lk[qq] >= 0 && ((lk[qq] < 2) != (lm[qq] < 2))) oflag |= 1u << qq;
     }
 
     // ---- helpers ----
@@ -598,9 +661,21 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     // gather_issue(node): the entries past the partials are pre-tagged there.
     constexpr int GNE = AME_GW * PW, GGE = (GNE + 127) / 128;
     uint64_t gv[GGE];
+    // raw y_{node,node-3}, y_{node,node-2} (threads ht < PW) and y_{node,node-1}
+    // (ht == 0), loaded with the partials: in phase 2 they were HBM round trips
+    // on the waves that signal the partials
+    float2 gy[3];
     auto gather_issue = [&](int node) {
         const int ht = tid - 128;
         if (ht < 0) return;
+        if (ht < PW) {
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const int j = node - 3 + q;
+                gy[q] = (j >= 0 && (q < 2 || ht == 0)) ? *(const float2*)(ysl + ((size_t)node * nys + j) * 2)
+                                                       : make_float2(0.f, 0.f);
+            }
+        }
         const uint32_t want = ame_gw_tag(a.epoch, node);
         const uint64_t* hp = (const uint64_t*)a.work + (size_t)tl * AME_GW * AME_GW_RING * PW;
         const uint64_t* hs = hp + (size_t)(node % AME_GW_RING) * PW;
@@ -653,10 +728,15 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         }
         if (ht < PW) {
             float acc = 0.f;
-            for (int j = node - 3; j <= node - 2; ++j) {
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int j = node - 3 + q;
                 if (j < 0) continue;
-                const float2 y = *(const float2*)(ysl + ((size_t)node * nys + j) * 2);
-                const float z0 = r00f * y.x + r01f * y.y, z1 = r10f * y.x + r11f * y.y;
+                const float2 y = gy[q];
+                // products rounded, then added: the compiler's contraction choice
+                // for a*b + c*d otherwise moves with the surrounding code
+                const float z0 = mul_add_rn(r00f, y.x, r01f, y.y);
+                const float z1 = mul_add_rn(r10f, y.x, r11f, y.y);
                 const float* mj = mring + (j & 3) * D;
                 if (ht < R) acc = fmaf(z0, mj[2 + R + ht], acc);          // h_U += z0 V
                 else if (ht < M2) acc = fmaf(z1, mj[2 + ht - R], acc);    // h_V += z1 U
@@ -665,29 +745,16 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             part[AME_GW * PW + ht] = acc;
         }
         if (ht == 0 && node >= 1) {
-            const float2 y = *(const float2*)(ysl + ((size_t)node * nys + node - 1) * 2);
-            scal[40] = (double)y.x;
-            scal[41] = (double)y.y;
+            scal[40] = (double)gy[2].x;
+            scal[41] = (double)gy[2].y;
         }
     };
-    // WK: the PhiTQi mu_right half first (mu_right is in LDS from phase 1 on),
-    // the QiPhi mu_left half once wave 1 has polled mu_left
-    auto ar_right = [&]() -> double {
-        double aR = 0.0;
-        if (at >= 0 && at < NPA * D) {
-            const int pp = at % NPA;
-            float mr[MC];
-#pragma unroll
-            for (int mm = 0; mm < MC; ++mm) {
-                const int m = pp * MC + mm;
-                mr[mm] = (m < D) ? mu_right[m] : 0.f;
-            }
-            double pR[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int mm = 0; mm < MC; ++mm) pR[mm & 3] = fma(phitqi[mm], (double)mr[mm], pR[mm & 3]);
-            aR = (pR[0] + pR[1]) + (pR[2] + pR[3]);
-        }
-        return aR;
+    // WK: the PhiTQi mu_right half of node `node`, precomputed before the sweep
+    // (ame_ar_right_kernel; the work buffer past the partial ring); the QiPhi
+    // mu_left half once wave 1 has polled mu_left
+    const double* arr = WK ? a.work + ame_v2_ring_doubles(&dm) + (size_t)tl * n * (NPA * D) : nullptr;
+    auto ar_right_load = [&](int node) -> double {
+        return (at >= 0 && at < NPA * D && node < n) ? arr[(size_t)node * (NPA * D) + at] : 0.0;
     };
     auto ar_left_finish = [&](int node, double aR) {
         if (at >= 0 && at < NPA * D) {
@@ -703,13 +770,13 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             for (int mm = 0; mm < MC; ++mm) pL[mm & 3] = fma(qiphi[mm], (double)ml[mm], pL[mm & 3]);
             const double aL = (pL[0] + pL[1]) + (pL[2] + pL[3]);
             double acc = ((tg > 0) ? aL : 0.0) + ((tg < Tt - 1) ? aR : 0.0);
-            acc += __shfl_xor(acc, 1);
-            if constexpr (NPA == 4) acc += __shfl_xor(acc, 2);
+            acc = ame::group_sum<NPA>(acc);
             if (pp == 0) gob(node)[D + k] = acc;
         }
     };
     auto ar_terms = [&](int node) {   // AR threads < NPA*D: QiPhi mu_left + PhiTQi mu_right
-        if (at >= 0 && at < NPA * D) {
+        if constexpr (WK) return;
+        else if (at >= 0 && at < NPA * D) {
             const int k = at / NPA, pp = at % NPA;
             // all LDS reads first, then two independent FMA chains
             float ml[MC], mr[MC];
@@ -728,8 +795,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             const double aL = (pL[0] + pL[1]) + (pL[2] + pL[3]);
             const double aR = (pR[0] + pR[1]) + (pR[2] + pR[3]);
             double acc = ((tg > 0) ? aL : 0.0) + ((tg < Tt - 1) ? aR : 0.0);
-            acc += __shfl_xor(acc, 1);
-            if constexpr (NPA == 4) acc += __shfl_xor(acc, 2);
+            acc = ame::group_sum<NPA>(acc);
             if (pp == 0) gob(node)[D + k] = acc;
         }
     };
@@ -805,27 +871,36 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     constexpr int NC4 = D * D / 4;                          // D is even
     constexpr int CQ = (NC4 + AME_NT - 1) / AME_NT;
     float4 cpf[CQ];
+    // rounds u < CF cover every thread (tid < AME_NT): only the last is masked.
+    // The flush reads every row from LDS before its first store (one round trip).
+    constexpr int CF = NC4 / AME_NT;
     auto cov_prefetch = [&](int node) {
         const float4* src = (const float4*)(cvs + (size_t)(node < n ? node : 0) * DD);
 #pragma unroll
         for (int u = 0; u < CQ; ++u) {
             const int e = tid + AME_NT * u;
-            cpf[u] = (e < NC4) ? src[e] : make_float4(0.f, 0.f, 0.f, 0.f);
+            cpf[u] = (u < CF || e < NC4) ? src[e] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
     auto cov_park = [&]() {
 #pragma unroll
         for (int u = 0; u < CQ; ++u) {
             const int e = tid + AME_NT * u;
-            if (e < NC4) ((float4*)cob)[e] = cpf[u];
+            if (u < CF || e < NC4) ((float4*)cob)[e] = cpf[u];
         }
     };
     auto cov_flush = [&](int node) {
         float4* dst = (float4*)(cvw + (size_t)node * DD);
+        float4 rows[CQ];
+#pragma unroll
+        for (int u = 0; u < CQ; ++u) {
+            const int e = min(tid + AME_NT * u, NC4 - 1);
+            rows[u] = ((const float4*)cst)[e];
+        }
 #pragma unroll
         for (int u = 0; u < CQ; ++u) {
             const int e = tid + AME_NT * u;
-            if (e < NC4) dst[e] = ((const float4*)cst)[e];
+            if (u < CF || e < NC4) dst[e] = rows[u];
         }
     };
     cov_prefetch(0);
@@ -865,7 +940,8 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     }
     __syncthreads();
     gemv_reduce(0);
-    ar_terms(0);
+    if constexpr (WK) ar_left_finish(0, ar_right_load(0));
+    else ar_terms(0);
     __syncthreads();
     // WK: the natural parameter's two parts (h_obs, AR terms) summed once into
     // gob(node)[k] (the K-matvec items of phase 1 read one value instead of two)
@@ -882,20 +958,24 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         // park first: waiting for last step's prefetch must not also wait for
         // this step's flush stores (vmcnt counts both, in order)
         cov_park();                      // old covariance of node i -> cob
+        STAMPW(16, 0);
         if (i >= 1) cov_flush(i - 1);   // staged by phase 3 of step i-1
         if (i + 1 < n) cov_prefetch(i + 1);
+        STAMPW(17, 0);
         // ---------------- phase 1 ----------------
-        // WK: node i+1's right-neighbour / old means and node i+2's old row load
-        // now and land in LDS at the end of phase 1, so phase 2 can start the AR
-        // terms before the worker partials arrive
-        float nx1 = 0.f, ol1 = 0.f, o21 = 0.f;
+        // WK: node i+1's old mean, its precomputed right AR term and node i+2's
+        // old row load now and land by the end of phase 1 / in phase 2
+        float ol1 = 0.f, o21 = 0.f;
+        double aR1 = 0.0;
         if constexpr (WK) {
             if (has_next) gather_issue(i + 1);
+            if (has_next) aR1 = ar_right_load(i + 1);
             if (has_next && tid >= 128 && tid < 128 + D) {
-                right_regs(i + 1, nx1, ol1);
+                ol1 = xo[(size_t)(i + 1) * D + (tid - 128)];
                 if (i + 2 < n) o21 = xo[(size_t)(i + 2) * D + (tid - 128)];
             }
         }
+        STAMPW(20, 128);
         if (has_prev && tid < M2) {   // node i-1: statistics and slice (U,V) <- new
             const double vo = (double)orow(i - 1)[tid], vn = (double)mu_prev[2 + tid];
             ssq[tid] = ssq[tid] - vo * vo + vn * vn;
@@ -919,13 +999,22 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 double p4[4] = {K[k * KS + (row0 ? 0 : 1)], 0.0, 0.0, 0.0};
                 if constexpr (R % 2 == 0) {
                     // the node vector as 8-byte pairs (it starts 8-byte aligned when
-                    // r is even): half the LDS read instructions, same sums
+                    // r is even): half the LDS read instructions, same sums.  Every
+                    // read is issued before the arithmetic: left to the scheduler,
+                    // each pair of reads waited for a full LDS round trip (one wave
+                    // per SIMD here, so nothing else hides it)
                     const float2* v2 = (const float2*)vv;
+                    float2 t[R / 2];
+                    double kv[R];
+#pragma unroll
+                    for (int c2 = 0; c2 < R / 2; ++c2) t[c2] = v2[c2];
+#pragma unroll
+                    for (int c = 0; c < R; ++c) kv[c] = kr[c];
+                    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                     for (int c2 = 0; c2 < R / 2; ++c2) {
-                        const float2 t = v2[c2];
-                        p4[(2 * c2) & 3] = fma(kr[2 * c2], (double)t.x, p4[(2 * c2) & 3]);
-                        p4[(2 * c2 + 1) & 3] = fma(kr[2 * c2 + 1], (double)t.y, p4[(2 * c2 + 1) & 3]);
+                        p4[(2 * c2) & 3] = fma(kv[2 * c2], (double)t[c2].x, p4[(2 * c2) & 3]);
+                        p4[(2 * c2 + 1) & 3] = fma(kv[2 * c2 + 1], (double)t[c2].y, p4[(2 * c2 + 1) & 3]);
                     }
                 } else {
 #pragma unroll
@@ -938,10 +1027,18 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 const int m0 = 2 + ch * 16;
                 const double* gi = gob(i);
                 double p2[2] = {0.0, 0.0};
+                double kv[16], gv2[16];   // reads first (see wy_item)
+#pragma unroll
+                for (int mm = 0; mm < 16; ++mm) {
+                    const int m = min(m0 + mm, D - 1);
+                    kv[mm] = K[k * KS + m];
+                    gv2[mm] = WK ? gi[m] : gi[m] + gi[D + m];
+                }
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int mm = 0; mm < 16; ++mm) {
                     const int m = m0 + mm;
-                    if (m < D) p2[mm & 1] = fma(K[k * KS + m], WK ? gi[m] : gi[m] + gi[D + m], p2[mm & 1]);
+                    if (m < D) p2[mm & 1] = fma(kv[mm], gv2[mm], p2[mm & 1]);
                 }
                 return p2[0] + p2[1];
             };
@@ -957,10 +1054,14 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 // the 8 W/Y items of rows 64, 65 into 8 column parts each, wave 1
                 // takes chunks 256..263, waves 2-3 the a-parts.
                 vec[(tid & 3) * D + (tid >> 2)] = wy_item(tid);
+                STAMPW(18, 0);
+                STAMPW(21, 128);
                 {
                     const int ch = tid / D;
                     vec[(5 + ch) * D + (tid - ch * D)] = chunk(tid);
                 }
+                STAMPW(19, 0);
+                STAMPW(22, 128);
                 if (wave == 0) {
                     const int it = 256 + (lane >> 3), pp = lane & 7;
                     double v = 0.0;
@@ -977,9 +1078,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                             v = p2[0] + p2[1];
                         }
                     }
-                    v += __shfl_xor(v, 1);
-                    v += __shfl_xor(v, 2);
-                    v += __shfl_xor(v, 4);
+                    v = ame::group_sum<8>(v);
                     if (pp == 0) vec[(it & 3) * D + (it >> 2)] = v;
                 } else if (wave == 1) {
                     // chunks 256..263 split 8 ways like wave 0's W/Y items (one
@@ -995,9 +1094,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                         const int m = m0 + mm;
                         if (m < D) v = fma(K[k * KS + m], WK ? gi[m] : gi[m] + gi[D + m], v);
                     }
-                    v += __shfl_xor(v, 1);
-                    v += __shfl_xor(v, 2);
-                    v += __shfl_xor(v, 4);
+                    v = ame::group_sum<8>(v);
                     if (pp == 0) vec[(5 + ch) * D + k] = v;
                 } else {
                     const int k = tid - 128;
@@ -1023,7 +1120,6 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         }
         if constexpr (WK) {
             if (has_next && tid >= 128 && tid < 128 + D) {
-                mu_right[tid - 128] = nx1;
                 mu_old_n[tid - 128] = ol1;
                 oring[((i + 2) & 3) * D + (tid - 128)] = o21;   // node i-2's slot: not read this step
             }
@@ -1033,6 +1129,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         if constexpr (MG) {
             if (wave == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
+        STAMPW(23, 128);
         lds_barrier();   // B1
         STAMP(1);
         // ---------------- phase 2 ----------------
@@ -1134,7 +1231,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 const int k = lane + 64 * h;
                 if (!is_naive) mus[h] += 1e-6 * hk[h];
                 if (k < D) {   // damped new mean; publish (mu_prev: readers above are done, wave-ordered)
-                    const float nw = __fadd_rn(__fmul_rn(lr, (float)mus[h]), __fmul_rn(om, mu_old[k]));
+                    const float nw = mul_add_rn(lr, (float)mus[h], om, mu_old[k]);
                     xn[(size_t)i * D + k] = nw;
                     if constexpr (MG) {
                         if (k >= 2) Mg[(size_t)i * M2 + (k - 2)] = nw;
@@ -1217,8 +1314,9 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             double aR = 0.0;
             if constexpr (WK) {
                 gather(i + 1);
-                aR = ar_right();   // mu_right landed in phase 1; after the gather, whose
-                                   // cross-CU loads set when waves 2-3 signal
+                STAMPW(24, 128);
+                aR = aR1;   // loaded in phase 1
+                STAMPW(25, 128);
             } else {
                 if (i + 2 < n) prefetch_y(i + 2);
                 gemv(tid - 64);
@@ -1243,6 +1341,8 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 ame::lds_wait_ge(wsync, 3u * (uint32_t)(i + 1), a.status, dead);
                 P2STAMP(6);
                 gemv_reduce(i + 1);
+                STAMPW(26, 64);
+                STAMPW(27, 128);
                 ar_left_finish(i + 1, aR);
                 P2STAMP(2 * (wave - 1) + 1);
             }
@@ -1254,47 +1354,56 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         // WK: node i+1's natural parameter in one piece (its parts were written
         // in phase 2, before B2; read from phase 1 of the next step on)
         if (WK && has_next && tid < D) gob(i + 1)[tid] += gob(i + 1)[D + tid];
+        STAMPW(28, 0);
         {
             // the LDS reads of QB rounds first, then their stores: a round's K / cst
             // stores otherwise keep the next round's reads behind them (the compiler
             // cannot tell the addresses apart), serialising the rounds.  Each
             // thread owns its (k, m) entries, and only k >= m is read.
-            constexpr int QB = 3;
+            // Branch-free: every round but the last has an entry on every
+            // thread (LTF full rounds); flags select the variant's value; a
+            // diagonal entry stores its (equal) mirror value twice.
+            constexpr int QB = 5;   // 9 entries per thread at d = 66: rounds of 5 and 4
+            constexpr int LTF = NLT / AME_NT;
+            // opaque per step: hoisted out of the loop, each flag test became a
+            // lane mask in an SGPR pair, spilled and reloaded per entry
+            uint32_t df = dflag, of = oflag;
+            asm volatile("" : "+v"(df), "+v"(of));
 #pragma unroll
             for (int q0 = 0; q0 < LTQ; q0 += QB) {
             double kr[QB], u0[QB], u1[QB], u2[QB], u3[QB], u4[QB], u5[QB], u6[QB], u7[QB];
-            float ckm[QB], cmk[QB];
+            float ckm[QB], cmk[QB], nd[QB];
 #pragma unroll
             for (int b = 0; b < QB; ++b) {
-                const int qq = q0 + b;
-                const bool ok = qq < LTQ && lk[qq < LTQ ? qq : 0] >= 0;
-                const int k = ok ? lk[qq] : 0, m = ok ? lm[qq] : 0;
+                const int qq = q0 + b < LTQ ? q0 + b : LTQ - 1;
+                const int k = max(lk[qq], 0), m = max(lm[qq], 0);
                 kr[b] = K[k * KS + m];
                 u0[b] = upd[k]; u1[b] = upd[2 * D + m]; u2[b] = upd[D + k]; u3[b] = upd[3 * D + m];
                 u4[b] = upd[4 * D + k]; u5[b] = upd[6 * D + m]; u6[b] = upd[5 * D + k]; u7[b] = upd[7 * D + m];
                 ckm[b] = cob[k * D + m];
                 cmk[b] = cob[m * D + k];
+                nd[b] = ndiag[k];   // naive only (C = diag(1 / (diag(P_i) + 1e-8)), formed in phase 2)
             }
 #pragma unroll
             for (int b = 0; b < QB; ++b) {
                 const int qq = q0 + b;
                 if (qq >= LTQ) continue;
-                const int k = lk[qq], m = lm[qq];
-                if (k < 0) continue;
+                const int k = max(lk[qq], 0), m = max(lm[qq], 0);
                 const double c = kr[b] - (u0[b] * u1[b] + u2[b] * u3[b]);
                 const double kn = c + (u4[b] * u5[b] + u6[b] * u7[b]);
-                K[k * KS + m] = kn;
-                K[m * KS + k] = kn;
-                float c32;
-                if (is_naive) {   // C = diag(1 / (diag(P_i) + 1e-8)), formed in phase 2
-                    c32 = (k == m) ? ndiag[k] : 0.f;
-                } else {
-                    c32 = (float)c;
-                    if (is_bad && ((k < 2) != (m < 2))) c32 = 0.f;
-                    if (k == m) c32 = c32 + 1e-6f;
+                const bool dg = (df >> qq) & 1u, ob = (of >> qq) & 1u;
+                float c32 = (float)c;
+                c32 = (is_bad && ob) ? 0.f : c32;
+                c32 = dg ? c32 + 1e-6f : c32;
+                c32 = is_naive ? (dg ? nd[b] : 0.f) : c32;
+                const float vkm = mul_add_rn(lr, c32, om, ckm[b]);
+                const float vmk = mul_add_rn(lr, c32, om, cmk[b]);
+                if (qq < LTF || lk[qq] >= 0) {
+                    K[k * KS + m] = kn;
+                    K[m * KS + k] = kn;
+                    cst[k * D + m] = vkm;
+                    cst[m * D + k] = vmk;
                 }
-                cst[k * D + m] = __fadd_rn(__fmul_rn(lr, c32), __fmul_rn(om, ckm[b]));
-                if (k != m) cst[m * D + k] = __fadd_rn(__fmul_rn(lr, c32), __fmul_rn(om, cmk[b]));
             }
             }
             STAMPW(14, 0);
@@ -1326,6 +1435,14 @@ static int launch_sweep_t(const ame_dims* dm, const ame_sweep_args* a, hipStream
         // partial ring: zero never matches a tag (ame_gw_tag sets bit 31)
         const size_t bytes = (size_t)ame_v2_ring_doubles(dm) * 8;
         if (hipMemsetAsync(a->work, 0, bytes, st) != hipSuccess) return -3;
+        static_assert(ArPart<R, true>::NPA == ((4 * (2 + 2 * R) <= 192) ? 4 : 2),
+                      "ame_v2_arr_doubles sizes the AR parts");
+        const long long nb = (long long)dm->T_local * dm->n;
+        if (nb > 0) {
+            hipLaunchKernelGGL(ame_ar_right_kernel<R>, dim3((unsigned)nb), dim3(AME_NT), 0, st, *dm, *a,
+                               a->work + ame_v2_ring_doubles(dm));
+            if (hipGetLastError() != hipSuccess) return -3;
+        }
     }
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(AME_NT), (size_t)lds, st, *dm, *a);
     return hipGetLastError() == hipSuccess ? 0 : -3;

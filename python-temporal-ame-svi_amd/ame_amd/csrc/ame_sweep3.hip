@@ -840,7 +840,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             if (kl) {
                 const float* xold = xring + (i & 7) * 64;
                 mold = xold[k];
-                nw = __fadd_rn(__fmul_rn(lr, (float)mus), __fmul_rn(om, mold));
+                nw = mul_add_rn(lr, (float)mus, om, mold);
                 xn[(size_t)i * D + k] = nw;
                 const uint64_t gr = ((uint64_t)a.epoch << 32) | (uint64_t)__float_as_uint(nw);
                 gran_store_agent(a.hand + ((size_t)tl * n + i) * D + k, gr);
@@ -967,8 +967,8 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                         if (is_bad && ((k < 2) != (m < 2))) c32 = 0.f;
                         if (k == m) c32 = c32 + 1e-6f;
                     }
-                    const float n_km = __fadd_rn(__fmul_rn(lr, c32), __fmul_rn(om, ckm));
-                    const float n_mk = __fadd_rn(__fmul_rn(lr, c32), __fmul_rn(om, cmk));
+                    const float n_km = mul_add_rn(lr, c32, om, ckm);
+                    const float n_mk = mul_add_rn(lr, c32, om, cmk);
                     if (ok && i < n) {
                         Kn[k * KS + m] = kn;
                         Kn[m * KS + k] = kn;

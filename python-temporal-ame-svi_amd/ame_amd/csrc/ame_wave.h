@@ -21,6 +21,27 @@ __device__ __forceinline__ uint32_t dpp_partner(uint32_t x) {
     else return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);
 }
 
+// Sum over aligned groups of G = 2, 4 or 8 lanes, left on every lane of the
+// group (DPP, no LDS round trip).  quad_perm 1032 pairs lanes differing in bit
+// 0; quad_perm 3210 then adds the other pair's sum, row_half_mirror the other
+// quad's: each step adds a partner holding the same partial sums an xor
+// exchange (__shfl_xor 1, 2, 4) would deliver, and + commutes exactly, so lane
+// results are bit-identical to the xor tree.
+template <int S>
+__device__ __forceinline__ double dpp_partner_d(double x) {
+    const uint64_t u = (uint64_t)__double_as_longlong(x);
+    const uint32_t lo = dpp_partner<S>((uint32_t)u), hi = dpp_partner<S>((uint32_t)(u >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+template <int G>
+__device__ __forceinline__ double group_sum(double v) {
+    static_assert(G == 2 || G == 4 || G == 8, "group_sum: G in {2, 4, 8}");
+    v += dpp_partner_d<5>(v);
+    if constexpr (G >= 4) v += dpp_partner_d<4>(v);
+    if constexpr (G >= 8) v += dpp_partner_d<3>(v);
+    return v;
+}
+
 // One pair step: lanes with bit==0 return A_own + A_partner, bit==1 lanes
 // return B_own + B_partner.
 template <int S>

@@ -56,7 +56,7 @@ def test_host_only_entry_points():
     # scratch of each concrete kind (host arithmetic, no device query)
     assert lib.ame_sweep_work_size(ctypes.byref(d), L.AME_SWEEP_V2_LDS) == 0
     assert lib.ame_sweep_work_size(ctypes.byref(d), L.AME_SWEEP_V2_HBM) == 128 * 1024 * 32 // 2
-    assert lib.ame_sweep_work_size(ctypes.byref(d), L.AME_SWEEP_V2_WORKERS) == 128 * 7 * 8 * 34
+    assert lib.ame_sweep_work_size(ctypes.byref(d), L.AME_SWEEP_V2_WORKERS) == 128 * 7 * 8 * 34 + 128 * 1024 * 4 * 34
     assert lib.ame_sweep_work_size(ctypes.byref(d), 2) == -1     # a request, not a kind
 
 

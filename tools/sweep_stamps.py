@@ -79,7 +79,7 @@ def run():
     torch.cuda.synchronize()
     L = _lib.lib()
     L.ame_debug_read_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    NPH = 16
+    NPH = 32
     buf = (ctypes.c_ulonglong * (16 * NPH))()
     assert L.ame_debug_read_stamps(buf, 16 * NPH) == 0
     rows = [[buf[k * NPH + p] for p in range(NPH)] for k in range(16)]
@@ -101,6 +101,13 @@ def run():
            10: "w0 multidot-2 done", 11: "w1 gemv done", 12: "w1 poll done",
            13: "w2 gemv done", 14: "w0 K update + cov write done", 15: "w0 gemv_reduce+AR done"}
     base = {4: 0, 5: 0, 6: 0, 7: 0, 8: 1, 9: 1, 10: 1, 11: 1, 12: 1, 13: 1, 14: 2, 15: 2}
+    if any(rows[k][16] for k in range(15)):   # fine slots (kind 22)
+        sub.update({16: "w0 cov park", 17: "w0 cov flush + prefetch issued", 18: "w0 W/Y item",
+                    19: "w0 chunk", 20: "w2 loads issued", 21: "w2 W/Y item", 22: "w2 chunk",
+                    23: "w2 right/old rows parked", 24: "w2 gather done", 25: "w2 ar_right",
+                    26: "w1 gemv_reduce", 27: "w2 gemv_reduce", 28: "w0 gob summed"})
+        base.update({16: 0, 17: 0, 18: 0, 19: 0, 20: 0, 21: 0, 22: 0, 23: 0, 24: 1, 25: 1,
+                     26: 1, 27: 1, 28: 2})
     for ph in sorted(sub):
         d = sum(rows[k][ph] - rows[k][base[ph]] for k in range(15)) / 15
         print(f"    +{d:8.0f} after phase start: {sub[ph]}")
