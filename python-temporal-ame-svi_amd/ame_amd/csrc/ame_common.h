@@ -47,16 +47,10 @@ __device__ __forceinline__ void gran_store_system(uint64_t* p, uint64_t v) {
 // z = R^-1 y).  __fadd_rn / __fmul_rn are plain + and * in this HIP, which
 // -ffp-contract=fast may fuse -- differently for a covariance entry and its
 // mirror, so the damped covariance was not exactly symmetric.
-#ifdef AME_EXP_FUSE
-__device__ __forceinline__ float mul_add_rn(float a, float b, float c, float d) {
-    return a * b + c * d;
-}
-#else
 __device__ __forceinline__ float mul_add_rn(float a, float b, float c, float d) {
 #pragma clang fp contract(off)
     return a * b + c * d;
 }
-#endif
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll

@@ -48,7 +48,12 @@ def _check_vs_oracle(n, T, r, method, lr, dev, iters=2, **opts):
     fp32_err = np.abs(Xm32.astype(np.float64) - Xm).max()
     h = vi.fit(max_iter=iters, tolerance=0.0, verbose=False)
     err = np.abs(vi.X_mean.numpy() - Xm).max()
-    assert err <= max(5e-6 * max(1.0, np.abs(Xm).max()), fp32_err), (err, fp32_err)
+    # fp32 allowance: twice the fp32 restatement's own deviation from fp64.  Two
+    # fp32 evaluations that differ only in rounding order land on either side of
+    # each other: on (64, 3, 8, good, 0.5) the kernel's error is 0.56x the fp32
+    # oracle's with the damping FMA-contracted and 1.11x with it rounded as the
+    # reference does (tools/parity_margin.py)
+    assert err <= max(5e-6 * max(1.0, np.abs(Xm).max()), 2.0 * fp32_err), (err, fp32_err)
     cerr = np.abs(vi.X_cov.numpy() - Xc).max()
     assert cerr <= 1e-6 * max(1.0, np.abs(Xc).max()), cerr
     for a, b in zip(h["elbo"], ref["elbo"]):
