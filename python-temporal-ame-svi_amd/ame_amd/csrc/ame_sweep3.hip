@@ -918,16 +918,6 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             lk[q] = k;
             lm[q] = m;
         }
-        // per-entry flags as bits of one register (bit q): diagonal entry, entry off
-        // the bad factorization's block diagonal.  Kept as lane masks they lived in
-        // SGPR pairs, which spill: a v_readlane pair per use in every step
-        uint32_t dflag = 0u, oflag = 0u;
-#pragma unroll
-        for (int q = 0; q < LTQ; ++q) {
-            if (lk[q] >= 0 && lk[q] == lm[q]) dflag |= 1u << q;
-            if (lk[q] >= 0 && ((lk[q] < 2) != (lm[q] < 2))) oflag |= 1u << q;
-        }
-        constexpr int LTF = NLT / C::NHB;   // rounds with an entry on every HB lane
         for (int i = 0; i <= n; ++i) {
             STAMP3(0);
             const int par = i & 1, ppar = (i + 1) & 1;
@@ -959,25 +949,24 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 const double* pdp = pdl + (size_t)ppar * D;
                 const float* co = cring + (size_t)((i + 3) & 3) * LY::cs;   // node i-1
                 float* cv = cst + (size_t)(i & 1) * LY::cs;                  // node i-1, staged
-                // branch-free per entry (flags select the variant's value; a
-                // diagonal entry stores its equal mirror value twice)
-                uint32_t df = dflag, of = oflag;
-                asm volatile("" : "+v"(df), "+v"(of));   // not hoisted as lane masks
 #pragma unroll
                 for (int q = 0; q < LTQ; ++q) {
-                    const bool ok = (q < LTF) || lk[q] >= 0;
-                    const int k = max(lk[q], 0), m = max(lm[q], 0);
+                    const bool ok = lk[q] >= 0;
+                    const int k = ok ? lk[q] : 0, m = ok ? lm[q] : 0;
                     const double* rk = rp + k * RS;
                     const double* rm = rp + m * RS;
                     const double bkm = Bi[k * KS + m];
                     const float ckm = co[k * D + m], cmk = co[m * D + k];
                     const double c = bkm - (rk[0] * rm[2] + rk[1] * rm[3]);
                     const double kn = c + (rk[4] * rm[6] + rk[5] * rm[7]);
-                    const bool dg = (df >> q) & 1u, ob = (of >> q) & 1u;
-                    float c32 = (float)c;
-                    c32 = (is_bad && ob) ? 0.f : c32;
-                    c32 = dg ? c32 + 1e-6f : c32;
-                    if (is_naive) c32 = dg ? 1.0f / ((float)pdp[k] + 1e-8f) : 0.f;
+                    float c32;
+                    if (is_naive) {
+                        c32 = (k == m) ? 1.0f / ((float)pdp[k] + 1e-8f) : 0.f;
+                    } else {
+                        c32 = (float)c;
+                        if (is_bad && ((k < 2) != (m < 2))) c32 = 0.f;
+                        if (k == m) c32 = c32 + 1e-6f;
+                    }
                     const float n_km = mul_add_rn(lr, c32, om, ckm);
                     const float n_mk = mul_add_rn(lr, c32, om, cmk);
                     if (ok && i < n) {
@@ -986,7 +975,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                     }
                     if (ok && i >= 1) {
                         cv[k * D + m] = n_km;
-                        cv[m * D + k] = n_mk;
+                        if (k != m) cv[m * D + k] = n_mk;
                     }
                 }
             }
