@@ -189,36 +189,51 @@ struct ArPart {
 // (fixed for the whole sweep), so the sweep reads one value per thread and
 // step instead of forming it on its critical path.  Same products, order and
 // zero padding as the in-sweep form (ar_terms), so the sums are unchanged.
-// One workgroup per (slice, node); out[(tl * n + j) * NPA * D + at].
+// A workgroup takes AR_NB nodes of one slice: their right means staged in LDS
+// (one barrier), each thread's coefficient row part held in registers, then
+// one dot per node.  out[(tl * n + j) * NPA * D + at].
+#define AR_NB 64
 template <int R>
 __global__ void __launch_bounds__(AME_NT)
 ame_ar_right_kernel(ame_dims dm, ame_sweep_args a, double* out) {
     using P = ArPart<R, true>;
     constexpr int D = P::D, NPA = P::NPA, MC = P::MC;
     const int n = dm.n, TL = dm.T_local, Tt = dm.T_total;
-    const int tl = (int)blockIdx.x / n, j = (int)blockIdx.x - tl * n;
+    const int nbk = (n + AR_NB - 1) / AR_NB;
+    const int tl = (int)blockIdx.x / nbk, j0 = ((int)blockIdx.x - tl * nbk) * AR_NB;
     const int tg = dm.t_begin + tl;
-    __shared__ float mr_s[D];
-    const int at = threadIdx.x;
-    if (at < D) {
-        float v = 0.f;
-        if (tg < Tt - 1)
-            v = (tl < TL - 1) ? a.x_old[((size_t)(tl + 1) * n + j) * D + at] : a.next_old[(size_t)j * D + at];
-        mr_s[at] = v;
+    const int cnt = min(AR_NB, n - j0);
+    __shared__ float mr_s[AR_NB * D];
+    if (tg < Tt - 1) {   // the last global slice has no right neighbour (next_old may be NULL)
+        const float* src = (tl < TL - 1) ? a.x_old + ((size_t)(tl + 1) * n + j0) * D
+                                         : a.next_old + (size_t)j0 * D;
+        for (int e = threadIdx.x; e < cnt * D; e += AME_NT) mr_s[e] = src[e];
+    } else {
+        for (int e = threadIdx.x; e < cnt * D; e += AME_NT) mr_s[e] = 0.f;
     }
-    __syncthreads();
-    if (at >= NPA * D) return;
-    const int k = at / NPA, pp = at % NPA;
+    const int at = threadIdx.x;
+    const bool act = at < NPA * D;
+    const int k = act ? at / NPA : 0, pp = at % NPA;
     const size_t DD = (size_t)D * D;
-    double pR[4] = {0.0, 0.0, 0.0, 0.0};
+    double c[MC];
 #pragma unroll
     for (int mm = 0; mm < MC; ++mm) {
         const int m = pp * MC + mm;
-        const double c = (m < D) ? a.consts[4 * DD + (size_t)k * D + m] : 0.0;
-        const float x = (m < D) ? mr_s[m] : 0.f;
-        pR[mm & 3] = fma(c, (double)x, pR[mm & 3]);
+        c[mm] = (m < D) ? a.consts[4 * DD + (size_t)k * D + m] : 0.0;
     }
-    out[((size_t)tl * n + j) * (NPA * D) + at] = (pR[0] + pR[1]) + (pR[2] + pR[3]);
+    __syncthreads();
+    if (!act) return;
+    for (int q = 0; q < cnt; ++q) {
+        const float* mr = mr_s + q * D;
+        double pR[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int mm = 0; mm < MC; ++mm) {
+            const int m = pp * MC + mm;
+            const float x = (m < D) ? mr[m] : 0.f;
+            pR[mm & 3] = fma(c[mm], (double)x, pR[mm & 3]);
+        }
+        out[((size_t)tl * n + j0 + q) * (NPA * D) + at] = (pR[0] + pR[1]) + (pR[2] + pR[3]);
+    }
 }
 
 // GEMV worker (MODE 2): workgroup TL + t*AME_GW + g owns nodes
@@ -1195,8 +1210,8 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 M22 Mi = inv22(Mm);
                 Mi.b = Mi.c = 0.5 * (Mi.b + Mi.c);
                 // rows 0, 1 of W (J K[:,b] = (W0[b], W1[b])) live in lanes 0, 1 of h = 0
-                const double Wa00 = __shfl(W0[0], 0), Wa01 = __shfl(W0[0], 1);
-                const double Wa10 = __shfl(W1[0], 0), Wa11 = __shfl(W1[0], 1);
+                const double Wa00 = ame::lane_bcast(W0[0], 0), Wa01 = ame::lane_bcast(W0[0], 1);
+                const double Wa10 = ame::lane_bcast(W1[0], 0), Wa11 = ame::lane_bcast(W1[0], 1);
 #pragma unroll
                 for (int h = 0; h < KH; ++h) {
                     const int k = lane + 64 * h;
@@ -1437,7 +1452,7 @@ static int launch_sweep_t(const ame_dims* dm, const ame_sweep_args* a, hipStream
         if (hipMemsetAsync(a->work, 0, bytes, st) != hipSuccess) return -3;
         static_assert(ArPart<R, true>::NPA == ((4 * (2 + 2 * R) <= 192) ? 4 : 2),
                       "ame_v2_arr_doubles sizes the AR parts");
-        const long long nb = (long long)dm->T_local * dm->n;
+        const long long nb = (long long)dm->T_local * ((dm->n + AR_NB - 1) / AR_NB);
         if (nb > 0) {
             hipLaunchKernelGGL(ame_ar_right_kernel<R>, dim3((unsigned)nb), dim3(AME_NT), 0, st, *dm, *a,
                                a->work + ame_v2_ring_doubles(dm));

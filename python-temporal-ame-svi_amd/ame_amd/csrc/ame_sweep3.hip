@@ -818,8 +818,8 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 const double KE0 = brow[0] - (Lp0 * rq[2] + Lp1 * rq[3]) + (Gp0 * rq[6] + Gp1 * rq[7]);
                 const double KE1 = brow[1] - (Lp0 * rq[RS + 2] + Lp1 * rq[RS + 3]) +
                                    (Gp0 * rq[RS + 6] + Gp1 * rq[RS + 7]);
-                const double WE00 = __shfl(W0, 0), WE01 = __shfl(W1, 0);   // W row 0
-                const double WE10 = __shfl(W0, 1), WE11 = __shfl(W1, 1);   // W row 1
+                const double WE00 = lane_bcast(W0, 0), WE01 = lane_bcast(W1, 0);   // W row 0
+                const double WE10 = lane_bcast(W0, 1), WE11 = lane_bcast(W1, 1);   // W row 1
                 const double wz0 = WE00 * zp0 + WE10 * zp1, wz1 = WE01 * zp0 + WE11 * zp1;
                 const double tA = uA + KE0 * zp0 + KE1 * zp1;
                 const V2 jA = {JuA.x + wz0, JuA.y + wz1};

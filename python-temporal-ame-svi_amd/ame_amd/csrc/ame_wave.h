@@ -21,6 +21,15 @@ __device__ __forceinline__ uint32_t dpp_partner(uint32_t x) {
     else return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);
 }
 
+// Lane l's value on every lane (v_readlane into SGPRs: no LDS round trip,
+// unlike __shfl's ds_bpermute); l is a compile-time or wave-uniform index.
+__device__ __forceinline__ double lane_bcast(double v, int l) {
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
 // Sum over aligned groups of G = 2, 4 or 8 lanes, left on every lane of the
 // group (DPP, no LDS round trip).  quad_perm 1032 pairs lanes differing in bit
 // 0; quad_perm 3210 then adds the other pair's sum, row_half_mirror the other
