@@ -86,11 +86,11 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* scratch /* 4*
 // updated this sweep, old ones after), and it takes no LDS.
 #define AME_LDS_MAX 163840LL
 struct SweepLds {
-    long long oK, oVec, oUpd, oRed, oScal, oG, oSsq, oF, oPart, oCst, oCob, oZ, oM, total;
+    long long oK, oVec, oUpd, oRed, oScal, oG, oSsq, oF, oPart, oCst, oCob, oZ, oV64, oM, total;
     int m_global;
 };
 __host__ __device__ inline long long ame_align16(long long x) { return (x + 15) & ~15LL; }
-__host__ __device__ inline SweepLds sweep_lds_layout(int n, int R, int force_global = 0) {
+__host__ __device__ inline SweepLds sweep_lds_layout(int n, int R, int force_global = 0, int wk = 0) {
     const int D = 2 + 2 * R, M2 = 2 * R, KS = D + 1, US = (M2 + 15) / 16;
     const int VEC = (R % 4 == 0) ? 4 : ((R % 2 == 0) ? 2 : 1);
     const int GW = 192 / (M2 / VEC);
@@ -107,7 +107,16 @@ __host__ __device__ inline SweepLds sweep_lds_layout(int n, int R, int force_glo
     L.oPart = o; o = ame_align16(o + 4LL * GW * (M2 + 2));
     L.oCst = o;  o = ame_align16(o + 4LL * D * D);   // new covariance of the step, staged
     L.oCob = o;  o = ame_align16(o + 4LL * D * D);   // old covariance of the step
-    L.oZ = o;    o = ame_align16(o + 8LL * (n > 2 * D ? n : 2 * D));   // z row, or (workers) new-mean ring
+    // z row; with workers only the 4-slot new-mean ring lives there
+    L.oZ = o;    o = ame_align16(o + (wk ? 16LL * D : 8LL * (n > 2 * D ? n : 2 * D)));
+    // (workers) fp64: mu_{i-1} and the old-row ring (phase 1's row dots), mu_{i+1,t-1}
+    // and QiPhi by AR row part (the AR-left sum of phase 2: LDS reads instead of
+    // coefficient registers)
+    L.oV64 = o;
+    if (wk) {
+        const int npa = (4 * D <= 192) ? 4 : 2, mcp = ((D + npa - 1) / npa + 1) & ~1;
+        o = ame_align16(o + 8LL * 6 * D + 8LL * D * npa * mcp);
+    }
     L.oM = o;
     const long long withM = ame_align16(o + 4LL * n * M2);
     L.m_global = (force_global || withM > AME_LDS_MAX) ? 1 : 0;
@@ -135,7 +144,7 @@ __host__ __device__ inline long long ame_v2_worker_lds(int n, int R) {
     return ame_align16(8LL * (NW > ZN ? NW : ZN)) + 4LL * 4 * (2 * R + 2);
 }
 __host__ __device__ inline long long ame_v2_mode_lds(int n, int R, int mode) {
-    const long long m = sweep_lds_layout(n, R, mode != 0 ? 1 : 0).total;
+    const long long m = sweep_lds_layout(n, R, mode != 0 ? 1 : 0, mode == 2 ? 1 : 0).total;
     if (mode != 2) return m;
     const long long w = ame_v2_worker_lds(n, R);
     return m > w ? m : w;

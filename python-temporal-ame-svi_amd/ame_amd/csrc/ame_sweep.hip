@@ -423,7 +423,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const bool is_naive = dm.variant == AME_NAIVE, is_bad = dm.variant == AME_BAD;
 
-    const SweepLds L = sweep_lds_layout(n, R, MODE != 0 ? 1 : 0);
+    const SweepLds L = sweep_lds_layout(n, R, MODE != 0 ? 1 : 0, WK ? 1 : 0);
     double* K = (double*)(smem + L.oK);          // D x KS
     double* vec = (double*)(smem + L.oVec);      // (5+US) x D  K-matvec results
     double* upd = (double*)(smem + L.oUpd);      // 8 x D       rank-4 update vectors
@@ -431,7 +431,9 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     double* scal = (double*)(smem + L.oScal);    // 64          sums / y_{i+1,i}
     double* gobs_b = (double*)(smem + L.oG);     // [node&1] {D g_obs, D AR terms}
     auto gob = [&](int node) { return gobs_b + (node & 1) * 2 * D; };
-    uint32_t* wsync = (uint32_t*)(scal + 60);    // WK: phase-2 signals of waves 1-3
+    // WK phase-2 signals: [0] the worker partials of node i+1 are in LDS (waves
+    // 2-3), [1] mu_{i+1,t-1} is in LDS (wave 1)
+    uint32_t* wsync = (uint32_t*)(scal + 60);
     double* ssq = (double*)(smem + L.oSsq);      // 2R          sum U^2, sum V^2 (naive diag)
     double* pcd = ssq + 2 * R;                   // D           diag of P_const
     float* ndiag = (float*)(pcd + D);            // D           naive: diag of the new covariance
@@ -444,6 +446,12 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     // step's single-node reads of old rows never wait on HBM
     float* oring = mu_prev + 5 * D;
     auto orow = [&](int j) -> const float* { return oring + (j & 3) * D + 2; };
+    // WK: fp64 copies of mu_{i-1,t}^new and of the old-row ring (phase 1's row dots
+    // read doubles: no conversions on the waves that run them)
+    double* mu_prev64 = WK ? (double*)(smem + L.oV64) : nullptr;
+    double* oring64 = WK ? mu_prev64 + D : nullptr;
+    double* mu_left64 = WK ? mu_prev64 + 5 * D : nullptr;   // wave 1's poll, fp64
+    double* qlds = WK ? mu_prev64 + 6 * D : nullptr;         // QiPhi [k][part][MCP]
     float* part = (float*)(smem + L.oPart);      // GW x PW   GEMV partials
     float* cst = (float*)(smem + L.oCst);        // D x D     new covariance of node i (phase 3)
     float* cob = (float*)(smem + L.oCob);        // D x D     old covariance of node i (phase 1)
@@ -492,7 +500,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         }
     }
     if (tid < D) pcd[tid] = pconst_entry(a.consts, D, tid, tid, tg, Tt);
-    if (tid == 0) *wsync = 0u;
+    if (tid == 0) wsync[0] = wsync[1] = 0u;
     __syncthreads();
     if (tid < M2) {   // sum of squares over all nodes: ssq[c<R] = sum U_c^2, ssq[R+c] = sum V_c^2
         double acc = 0.0;
@@ -555,15 +563,24 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     const int at = WK ? tid - 64 : tid;   // AR thread index
     // AR rows: thread (k = at / NPA, part = at % NPA); WK reads the PhiTQi half
     // precomputed (ame_ar_right_kernel)
-    double qiphi[MC], phitqi[WK ? 1 : MC];
-    {
+    // WK keeps QiPhi in LDS by row part (MCP: MC padded to even, 16-B rows)
+    constexpr int MCP = (MC + 1) & ~1;
+    double qiphi[WK ? 1 : MC], phitqi[WK ? 1 : MC];
+    if constexpr (WK) {
+        for (int e = tid; e < D * NPA * MCP; e += AME_NT) {
+            const int k = e / (NPA * MCP), r2 = e - k * (NPA * MCP), pp = r2 / MCP, mm = r2 - pp * MCP;
+            const int m = pp * MC + mm;
+            qlds[e] = (mm < MC && m < D) ? a.consts[3 * DD + (size_t)k * D + m] : 0.0;
+        }
+        for (int e = tid; e < D; e += AME_NT) mu_left64[e] = 0.0;
+    } else {
         const int k = at / NPA, pp = at % NPA;
 #pragma unroll
         for (int mm = 0; mm < MC; ++mm) {
             const int m = pp * MC + mm;
             const bool ok = (at >= 0) && (at < NPA * D) && (m < D);
             qiphi[mm] = ok ? a.consts[3 * DD + (size_t)k * D + m] : 0.0;
-            if constexpr (!WK) phitqi[mm] = ok ? a.consts[4 * DD + (size_t)k * D + m] : 0.0;
+            phitqi[mm] = ok ? a.consts[4 * DD + (size_t)k * D + m] : 0.0;
         }
     }
     int lk[LTQ], lm[LTQ];   // lower-triangle entries owned for the update / cov write
@@ -655,8 +672,10 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             }
         }
     };
-    auto gemv_reduce = [&](int node) {   // threads (WK: 64 +) < PW -> g_obs of node
-        const int rt = WK ? tid - 64 : tid;
+    auto gemv_reduce = [&](int node) {   // threads < PW -> g_obs of node
+        // WK: wave 3 (few AR items, gathers early) takes rt < 64, wave 1's first
+        // lanes the rest (rt 64, 65 at d = 66); wave 2 gathers and runs 64 AR items
+        const int rt = WK ? (tid >= 192 ? tid - 192 : ((tid >= 64 && tid < 64 + PW - 64) ? tid : -1)) : tid;
         if (rt >= 0 && rt < PW) {
             float acc = 0.f;
             for (int g = 0; g < (WK ? AME_GW + 1 : GW); ++g) acc += part[g * PW + rt];
@@ -680,26 +699,30 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     // (ht == 0), loaded with the partials: in phase 2 they were HBM round trips
     // on the waves that signal the partials
     float2 gy[3];
+    // per-thread ring offsets of the partial entries this thread gathers (fixed
+    // for the sweep); entries past the GNE real ones load entry 0 and are
+    // pre-tagged after the load (no branch, no per-step division)
+    int goff[GGE];
+    uint32_t gvalid = 0u;
+#pragma unroll
+    for (int u = 0; u < GGE; ++u) {
+        const int e = max(tid - 128, 0) + 128 * u, g = e / PW, c = e - g * PW;
+        goff[u] = (e < GNE) ? g * AME_GW_RING * PW + c : 0;
+        if (e < GNE) gvalid |= 1u << u;
+    }
     auto gather_issue = [&](int node) {
         const int ht = tid - 128;
         if (ht < 0) return;
         if (ht < PW) {
+            // y_{node, node-3+q}, column clamped to >= 0 (gather ignores j < 0).
+            // Raw loads only: a select on a loaded value here would wait for it
+            const float2* yr = (const float2*)(ysl + (size_t)node * nys * 2);
 #pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                const int j = node - 3 + q;
-                gy[q] = (j >= 0 && (q < 2 || ht == 0)) ? *(const float2*)(ysl + ((size_t)node * nys + j) * 2)
-                                                       : make_float2(0.f, 0.f);
-            }
+            for (int q = 0; q < 3; ++q) gy[q] = yr[max(node - 3 + q, 0)];
         }
-        const uint32_t want = ame_gw_tag(a.epoch, node);
-        const uint64_t* hp = (const uint64_t*)a.work + (size_t)tl * AME_GW * AME_GW_RING * PW;
-        const uint64_t* hs = hp + (size_t)(node % AME_GW_RING) * PW;
+        const uint64_t* hs = (const uint64_t*)a.work + ((size_t)tl * AME_GW * AME_GW_RING + (node % AME_GW_RING)) * PW;
 #pragma unroll
-        for (int u = 0; u < GGE; ++u) {
-            const int e = ht + 128 * u, g = e / PW, c = e - g * PW;
-            gv[u] = (e < GNE) ? gran_load_agent(hs + (size_t)g * AME_GW_RING * PW + c)
-                              : ((uint64_t)want << 32);
-        }
+        for (int u = 0; u < GGE; ++u) gv[u] = gran_load_agent(hs + goff[u]);
     };
     auto gather = [&](int node) {
         const int ht = tid - 128;
@@ -711,7 +734,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         uint64_t (&v)[GE] = gv;   // issued by gather_issue(node)
         bool ok = true;
 #pragma unroll
-        for (int u = 0; u < GE; ++u) ok = ok && (uint32_t)(v[u] >> 32) == want;
+        for (int u = 0; u < GE; ++u) ok = ok && (!((gvalid >> u) & 1u) || (uint32_t)(v[u] >> 32) == want);
         if (!ok && !dead) {
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             while (true) {
@@ -719,9 +742,8 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 ok = true;
 #pragma unroll
                 for (int u = 0; u < GE; ++u) {
-                    const int e = ht + 128 * u, g = e / PW, c = e - g * PW;
-                    if ((uint32_t)(v[u] >> 32) != want) {
-                        v[u] = gran_load_agent(hs + (size_t)g * AME_GW_RING * PW + c);
+                    if (((gvalid >> u) & 1u) && (uint32_t)(v[u] >> 32) != want) {
+                        v[u] = gran_load_agent(hs + goff[u]);
                         ok = ok && (uint32_t)(v[u] >> 32) == want;
                     }
                 }
@@ -759,7 +781,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             }
             part[AME_GW * PW + ht] = acc;
         }
-        if (ht == 0 && node >= 1) {
+        if (ht == 0 && node >= 1) {   // j = node - 1 >= 0
             scal[40] = (double)gy[2].x;
             scal[41] = (double)gy[2].y;
         }
@@ -774,15 +796,22 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     auto ar_left_finish = [&](int node, double aR) {
         if (at >= 0 && at < NPA * D) {
             const int k = at / NPA, pp = at % NPA;
-            float ml[MC];
+            // WK: coefficients and mu_left from LDS (fp64), every read first
+            const double* qr = qlds + (size_t)at * MCP;
+            double cq[MC], ml[MC];
 #pragma unroll
             for (int mm = 0; mm < MC; ++mm) {
                 const int m = pp * MC + mm;
-                ml[mm] = (m < D) ? mu_left[m] : 0.f;
+                cq[mm] = qr[mm];
+                ml[mm] = mu_left64[m < D ? m : D - 1];
             }
+            __builtin_amdgcn_sched_barrier(0);
             double pL[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int mm = 0; mm < MC; ++mm) pL[mm & 3] = fma(qiphi[mm], (double)ml[mm], pL[mm & 3]);
+            for (int mm = 0; mm < MC; ++mm) {
+                const int m = pp * MC + mm;
+                pL[mm & 3] = fma(cq[mm], (m < D) ? ml[mm] : 0.0, pL[mm & 3]);
+            }
             const double aL = (pL[0] + pL[1]) + (pL[2] + pL[3]);
             double acc = ((tg > 0) ? aL : 0.0) + ((tg < Tt - 1) ? aR : 0.0);
             acc = ame::group_sum<NPA>(acc);
@@ -853,7 +882,10 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         }
 #pragma unroll
         for (int h = 0; h < KH; ++h)
-            if (lane + 64 * h < D) mu_left[lane + 64 * h] = __uint_as_float((uint32_t)v[h]);
+            if (lane + 64 * h < D) {
+                mu_left[lane + 64 * h] = __uint_as_float((uint32_t)v[h]);
+                if constexpr (WK) mu_left64[lane + 64 * h] = (double)__uint_as_float((uint32_t)v[h]);
+            }
     };
     auto first_poll = [&](int node, uint64_t (&g)[KH]) {   // wave 1: issue the first granule loads
         const bool from_halo = (tl == 0);
@@ -869,7 +901,10 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     auto zero_left = [&]() {   // wave 1, global slice 0: no left neighbour
 #pragma unroll
         for (int h = 0; h < KH; ++h)
-            if (lane + 64 * h < D) mu_left[lane + 64 * h] = 0.f;
+            if (lane + 64 * h < D) {
+                mu_left[lane + 64 * h] = 0.f;
+                if constexpr (WK) mu_left64[lane + 64 * h] = 0.0;
+            }
     };
     auto right_regs = [&](int node, float& nx, float& ol) {   // threads 128..128+D
         const int k = tid - 128;
@@ -942,6 +977,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         for (int e = tid; e < 2 * D; e += AME_NT) {
             const int j = e / D, k = e - j * D;
             oring[j * D + k] = (j < n) ? xo[(size_t)j * D + k] : 0.f;
+            if constexpr (WK) oring64[j * D + k] = (double)oring[j * D + k];
         }
     }
     if (!WK && n > 1) prefetch_y(1);
@@ -978,17 +1014,15 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         if (i + 1 < n) cov_prefetch(i + 1);
         STAMPW(17, 0);
         // ---------------- phase 1 ----------------
-        // WK: node i+1's old mean, its precomputed right AR term and node i+2's
-        // old row load now and land by the end of phase 1 / in phase 2
-        float ol1 = 0.f, o21 = 0.f;
+        // WK: node i+1's partials, Y entries and precomputed right AR term (read
+        // in phase 2) and node i+2's old row (parked in the old-row ring at the
+        // end of phase 3) load now; node i's old mean is read from that ring
+        float o21 = 0.f;
         double aR1 = 0.0;
         if constexpr (WK) {
             if (has_next) gather_issue(i + 1);
             if (has_next) aR1 = ar_right_load(i + 1);
-            if (has_next && tid >= 128 && tid < 128 + D) {
-                ol1 = xo[(size_t)(i + 1) * D + (tid - 128)];
-                if (i + 2 < n) o21 = xo[(size_t)(i + 2) * D + (tid - 128)];
-            }
+            if (has_next && tid >= 128 && tid < 128 + D && i + 2 < n) o21 = xo[(size_t)(i + 2) * D + (tid - 128)];
         }
         STAMPW(20, 128);
         if (has_prev && tid < M2) {   // node i-1: statistics and slice (U,V) <- new
@@ -1062,7 +1096,95 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 if constexpr (WK) return K[k * KS + 0] * gi[0] + K[k * KS + 1] * gi[1];
                 return K[k * KS + 0] * (gi[0] + gi[D]) + K[k * KS + 1] * (gi[1] + gi[D + 1]);
             };
-            if constexpr (R == 32 && AME_NT == 256) {
+            if constexpr (WK) {
+                // One pass over K per step (round 4): the W/Y items and u chunks
+                // read rows of K once per vector; here thread (k, h) takes row
+                // k >= 2, columns 2 + hR .. 2 + hR + R (the V half for h = 0, the
+                // U half for h = 1) and forms all three dots over them -- J0 / J1
+                // of node i-1 (W), of node i+1 (Y) and g (u) -- from fp64 copies
+                // of the vectors; rows 0 and 1 take one column per lane on waves
+                // 2 and 3 with a wave reduce-scatter.  Every read before the
+                // arithmetic.
+                const double* gi = gob(i);
+                const double* on64 = oring64 + ((i + 1) & 3) * D;   // node i+1, old (slot valid for any i)
+                // waves 0-1: lane l of wave w takes row 2 + 32 w + (l & 31), half
+                // h = l >> 5.  The halves of a row sit 2R dwords apart, on the same
+                // LDS banks, so they go to different 32-lane groups; within a group
+                // the 32 rows (stride KS = D + 1 doubles) cover all 64 banks
+                const int kk = 32 * wave + (lane & 31);
+                if (wave < 2 && kk < M2) {
+                    const int k = 2 + kk, h = lane >> 5;
+                    const double* kr = K + k * KS + 2 + h * R;
+                    const double* pj = mu_prev64 + 2 + (h ? 0 : R);   // J0: V (at 2+R), J1: U (at 2)
+                    const double* nj = on64 + 2 + (h ? 0 : R);
+                    const double* gg = gi + 2 + h * R;
+                    // the row part first (R reads), then the vectors in blocks of 8
+                    // columns, each block's reads before its arithmetic (register
+                    // budget: all four R-vectors at once would spill)
+                    double kv[R];
+#pragma unroll
+                    for (int c = 0; c < R; ++c) kv[c] = kr[c];
+                    const double kb = K[k * KS + h], k0 = K[k * KS], k1 = K[k * KS + 1];
+                    double w[4] = {0.0, 0.0, 0.0, 0.0}, y[4] = {0.0, 0.0, 0.0, 0.0}, u[4] = {0.0, 0.0, 0.0, 0.0};
+                    constexpr int CB = 8;
+#pragma unroll
+                    for (int c0 = 0; c0 < R; c0 += CB) {
+                        double pv[CB], nv[CB], gv[CB];
+#pragma unroll
+                        for (int b = 0; b < CB; ++b) {
+                            const int c = c0 + b < R ? c0 + b : R - 1;
+                            pv[b] = pj[c];
+                            nv[b] = nj[c];
+                            gv[b] = gg[c];
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int b = 0; b < CB; ++b) {
+                            const int c = c0 + b;
+                            if (c < R) {
+                                w[c & 3] = fma(kv[c], pv[b], w[c & 3]);
+                                y[c & 3] = fma(kv[c], nv[b], y[c & 3]);
+                                u[c & 3] = fma(kv[c], gv[b], u[c & 3]);
+                            }
+                        }
+                    }
+                    const double W = kb + ((w[0] + w[1]) + (w[2] + w[3]));
+                    const double Y = kb + ((y[0] + y[1]) + (y[2] + y[3]));
+                    const double uh = (u[0] + u[1]) + (u[2] + u[3]);
+                    const double U = ame::pair_step<0>(uh, uh, false);   // + the other half (lane l ^ 32)
+                    vec[h * D + k] = has_prev ? W : 0.0;
+                    vec[(2 + h) * D + k] = has_next ? Y : 0.0;
+                    if (h == 0) {
+                        vec[4 * D + k] = k0 * gi[0] + k1 * gi[1];
+                        vec[5 * D + k] = U;
+                    }
+                } else if (wave >= 2) {
+                    // rows 0 (wave 2) and 1 (wave 3): lane c takes column 2 + c
+                    const int r = (tid >= 192) ? 1 : 0, c = lane;
+                    const bool in = c < M2, hv = c >= R;   // hv: U half (J1)
+                    const int cm = in ? c : 0;
+                    const int src = 2 + (hv ? cm - R : cm + R);
+                    const double kv = in ? K[r * KS + 2 + cm] : 0.0;
+                    const double pv = in ? mu_prev64[src] : 0.0;
+                    const double nv = in ? on64[src] : 0.0;
+                    const double gv = in ? gi[2 + cm] : 0.0;
+                    double v5[5] = {hv ? 0.0 : kv * pv, hv ? kv * pv : 0.0, hv ? 0.0 : kv * nv, hv ? kv * nv : 0.0,
+                                    kv * gv};
+                    int idx;
+                    const double sv = ame::wave_reduce_scatter<5>(v5, lane, idx);
+                    if (idx < 5) {
+                        const double kb0 = K[r * KS], kb1 = K[r * KS + 1];
+                        if (idx == 0) vec[r] = has_prev ? kb0 + sv : 0.0;
+                        else if (idx == 1) vec[D + r] = has_prev ? kb1 + sv : 0.0;
+                        else if (idx == 2) vec[2 * D + r] = has_next ? kb0 + sv : 0.0;
+                        else if (idx == 3) vec[3 * D + r] = has_next ? kb1 + sv : 0.0;
+                        else {
+                            vec[5 * D + r] = sv;
+                            vec[4 * D + r] = kb0 * gi[0] + kb1 * gi[1];
+                        }
+                    }
+                }
+            } else if constexpr (R == 32 && AME_NT == 256) {
                 // d = 66: 264 W/Y items, 264 chunks, 66 a-parts.  Every round is
                 // one item type per wave (divergent item types in one wave run
                 // back to back): W/Y 0..255, chunks 0..255, then wave 0 splits
@@ -1133,12 +1255,6 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             if (!WK && has_next) stage_z(i + 1, i);
             STAMPW(7, 0);
         }
-        if constexpr (WK) {
-            if (has_next && tid >= 128 && tid < 128 + D) {
-                mu_old_n[tid - 128] = ol1;
-                oring[((i + 2) & 3) * D + (tid - 128)] = o21;   // node i-2's slot: not read this step
-            }
-        }
         // MG: node i-1's (U,V) row (stored by wave 0 in the previous step) is
         // read by this step's GEMV in waves 1-3: drain it before the barrier
         if constexpr (MG) {
@@ -1161,8 +1277,12 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 if (k < D) {
                     W0[h] = vec[k]; W1[h] = vec[D + k]; Y0[h] = vec[2 * D + k]; Y1[h] = vec[3 * D + k];
                     ua[h] = vec[4 * D + k];
+                    if constexpr (WK) {
+                        uM[h] = vec[5 * D + k];   // one (U,V) sum per row (phase 1)
+                    } else {
 #pragma unroll
-                    for (int ch = 0; ch < US; ++ch) uM[h] += vec[(5 + ch) * D + k];
+                        for (int ch = 0; ch < US; ++ch) uM[h] += vec[(5 + ch) * D + k];
+                    }
                     gk[h] = WK ? gob(i)[k] : gob(i)[k] + gob(i)[D + k];
                     K0[h] = K[k * KS + 0];
                     K1[h] = K[k * KS + 1];
@@ -1246,12 +1366,14 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 const int k = lane + 64 * h;
                 if (!is_naive) mus[h] += 1e-6 * hk[h];
                 if (k < D) {   // damped new mean; publish (mu_prev: readers above are done, wave-ordered)
-                    const float nw = mul_add_rn(lr, (float)mus[h], om, mu_old[k]);
+                    const float mo = WK ? oring[(i & 3) * D + k] : mu_old[k];   // node i, old
+                    const float nw = mul_add_rn(lr, (float)mus[h], om, mo);
                     xn[(size_t)i * D + k] = nw;
                     if constexpr (MG) {
                         if (k >= 2) Mg[(size_t)i * M2 + (k - 2)] = nw;
                     }
                     mu_prev[k] = nw;
+                    if constexpr (WK) mu_prev64[k] = (double)nw;
                     if constexpr (WK) mring[(i & 3) * D + k] = nw;
                     const uint64_t g = ((uint64_t)a.epoch << 32) | (uint64_t)__float_as_uint(nw);
                     gran_store_agent(a.hand + ((size_t)tl * n + i) * D + k, g);
@@ -1349,16 +1471,19 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 oring[((i + 2) & 3) * D + (tid - 128)] = o2;   // node i-2's slot: not read this step
             }
             if constexpr (WK) {
-                // partials, mu_{i+1,t-1} and mu_{i+1,t+1} are in LDS once waves 1-3
-                // have signalled: g_obs and the AR terms of node i+1, off phase 3
+                // g_obs and the AR terms of node i+1, off phase 3.  The AR terms
+                // need only mu_{i+1,t-1} (wave 1's poll), the g_obs sum only the
+                // partials (waves 2-3's gather): two signals, so each starts as
+                // soon as its input is in LDS
                 P2STAMP(2 * (wave - 1));
-                if (lane == 0) ame::lds_signal_add(wsync, 1u);
-                ame::lds_wait_ge(wsync, 3u * (uint32_t)(i + 1), a.status, dead);
+                if (lane == 0) ame::lds_signal_add(wave == 1 ? wsync + 1 : wsync, 1u);
+                ame::lds_wait_ge(wsync + 1, (uint32_t)(i + 1), a.status, dead);
+                ar_left_finish(i + 1, aR);
                 P2STAMP(6);
+                ame::lds_wait_ge(wsync, 2u * (uint32_t)(i + 1), a.status, dead);
                 gemv_reduce(i + 1);
                 STAMPW(26, 64);
                 STAMPW(27, 128);
-                ar_left_finish(i + 1, aR);
                 P2STAMP(2 * (wave - 1) + 1);
             }
         }
@@ -1427,7 +1552,15 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 ar_terms(i + 1);
             }
             STAMPW(15, 0);
-            if (tid >= 128 && tid < 128 + D) mu_old[tid - 128] = mu_old_n[tid - 128];
+            if constexpr (WK) {
+                // node i+2's old row into node i-2's ring slot (not read this step)
+                if (has_next && tid >= 128 && tid < 128 + D) {
+                    oring[((i + 2) & 3) * D + (tid - 128)] = o21;
+                    oring64[((i + 2) & 3) * D + (tid - 128)] = (double)o21;
+                }
+            } else {
+                if (tid >= 128 && tid < 128 + D) mu_old[tid - 128] = mu_old_n[tid - 128];
+            }
             y_prev0 = (float)scal[40];
             y_prev1 = (float)scal[41];
         }

@@ -115,7 +115,7 @@ def run():
         L.ame_debug_read_p2stamps.argtypes = [ctypes.c_void_p]
         pb = (ctypes.c_ulonglong * (16 * 8))()
         if L.ame_debug_read_p2stamps(pb) == 0 and pb[0]:
-            names = {0: "w1 signalled", 2: "w2 signalled", 4: "w3 signalled", 6: "sync passed (last wave)",
+            names = {0: "w1 signalled", 2: "w2 signalled", 4: "w3 signalled", 6: "AR-left done (last wave)",
                      1: "w1 reduce+AR done", 3: "w2 reduce+AR done", 5: "w3 reduce+AR done"}
             for sl in sorted(names):
                 d = sorted(pb[k * 8 + sl] - rows[k][1] for k in range(15))[7]
