@@ -74,7 +74,7 @@ __device__ unsigned long long g_ame_wstamps[16 * 8];
         }                                                                                  \
     } while (0)
 // phase-2 detail of the middle slice's waves 1-3 (WK): slot = 2 * wave-1 + {0: signalled, 1: reduce+AR done}
-__device__ unsigned long long g_ame_p2stamps[16 * 8];
+__device__ unsigned long long g_ame_p2stamps[16 * 16];
 #define P2STAMP(sl)                                                                        \
     do {                                                                                   \
         if (stamp_on && lane == 0) {                                                       \
@@ -82,7 +82,7 @@ __device__ unsigned long long g_ame_p2stamps[16 * 8];
             __builtin_amdgcn_sched_barrier(0);                                             \
             asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");     \
             __builtin_amdgcn_sched_barrier(0);                                             \
-            g_ame_p2stamps[(i - AME_STAMP_I0) * 8 + (sl)] = t_;                             \
+            g_ame_p2stamps[(i - AME_STAMP_I0) * 16 + (sl)] = t_;                            \
         }                                                                                  \
     } while (0)
 extern "C" int ame_debug_read_p2stamps(unsigned long long* host) {
@@ -163,6 +163,17 @@ __device__ __forceinline__ M22 inv22(M22 m) {
     const double id = 1.0 / (m.a * m.d - m.b * m.c);
     return {m.d * id, -m.b * id, -m.c * id, m.a * id};
 }
+// Per-step 2x2 inverses of wave 0's Woodbury chain: the determinant's
+// reciprocal from v_rcp_f64 plus two Newton steps (as the v3 solver) -- a
+// shorter dependent chain than the IEEE division sequence, full fp64 accuracy
+// for these well-scaled determinants
+__device__ __forceinline__ M22 inv22_fast(M22 m) {
+    const double det = m.a * m.d - m.b * m.c;
+    double r = __builtin_amdgcn_rcp(det);
+    r = fma(r, fma(-det, r, 1.0), r);
+    r = fma(r, fma(-det, r, 1.0), r);
+    return {m.d * r, -m.b * r, -m.c * r, m.a * r};
+}
 
 // lower-triangle index e -> (k, m), m <= k
 __device__ __forceinline__ void tri_decode(int e, int& k, int& m) {
@@ -183,58 +194,6 @@ struct ArPart {
     static constexpr int NPA = (4 * D <= ART) ? 4 : 2;
     static constexpr int MC = (D + NPA - 1) / NPA;
 };
-
-// MODE 2 (GEMV workers): the right-neighbour AR term PhiTQi mu_{j,t+1}^old of
-// every node j, per AR thread part, before the sweep.  Its inputs are old means
-// (fixed for the whole sweep), so the sweep reads one value per thread and
-// step instead of forming it on its critical path.  Same products, order and
-// zero padding as the in-sweep form (ar_terms), so the sums are unchanged.
-// A workgroup takes AR_NB nodes of one slice: their right means staged in LDS
-// (one barrier), each thread's coefficient row part held in registers, then
-// one dot per node.  out[(tl * n + j) * NPA * D + at].
-#define AR_NB 64
-template <int R>
-__global__ void __launch_bounds__(AME_NT)
-ame_ar_right_kernel(ame_dims dm, ame_sweep_args a, double* out) {
-    using P = ArPart<R, true>;
-    constexpr int D = P::D, NPA = P::NPA, MC = P::MC;
-    const int n = dm.n, TL = dm.T_local, Tt = dm.T_total;
-    const int nbk = (n + AR_NB - 1) / AR_NB;
-    const int tl = (int)blockIdx.x / nbk, j0 = ((int)blockIdx.x - tl * nbk) * AR_NB;
-    const int tg = dm.t_begin + tl;
-    const int cnt = min(AR_NB, n - j0);
-    __shared__ float mr_s[AR_NB * D];
-    if (tg < Tt - 1) {   // the last global slice has no right neighbour (next_old may be NULL)
-        const float* src = (tl < TL - 1) ? a.x_old + ((size_t)(tl + 1) * n + j0) * D
-                                         : a.next_old + (size_t)j0 * D;
-        for (int e = threadIdx.x; e < cnt * D; e += AME_NT) mr_s[e] = src[e];
-    } else {
-        for (int e = threadIdx.x; e < cnt * D; e += AME_NT) mr_s[e] = 0.f;
-    }
-    const int at = threadIdx.x;
-    const bool act = at < NPA * D;
-    const int k = act ? at / NPA : 0, pp = at % NPA;
-    const size_t DD = (size_t)D * D;
-    double c[MC];
-#pragma unroll
-    for (int mm = 0; mm < MC; ++mm) {
-        const int m = pp * MC + mm;
-        c[mm] = (m < D) ? a.consts[4 * DD + (size_t)k * D + m] : 0.0;
-    }
-    __syncthreads();
-    if (!act) return;
-    for (int q = 0; q < cnt; ++q) {
-        const float* mr = mr_s + q * D;
-        double pR[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int mm = 0; mm < MC; ++mm) {
-            const int m = pp * MC + mm;
-            const float x = (m < D) ? mr[m] : 0.f;
-            pR[mm & 3] = fma(c[mm], (double)x, pR[mm & 3]);
-        }
-        out[((size_t)tl * n + j0 + q) * (NPA * D) + at] = (pR[0] + pR[1]) + (pR[2] + pR[3]);
-    }
-}
 
 // GEMV worker (MODE 2): workgroup TL + t*AME_GW + g owns nodes
 // [g*NW, (g+1)*NW) of slice t, NW = ceil(n / AME_GW); wave q holds nodes
@@ -266,6 +225,50 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
     const float r00f = (float)a.rinv[0], r01f = (float)a.rinv[1], r10f = (float)a.rinv[2], r11f = (float)a.rinv[3];
     const bool col = lane < M2;
     bool dead = false;
+    // Right-neighbour AR terms PhiTQi mu_{j,t+1}^old of this worker's nodes, for
+    // the slice workgroup's phase 2 (same products, order and zero padding as
+    // its in-sweep form): formed here, before partial 0, and released with it --
+    // the slice reads them only after it has seen every worker's partial 0 and
+    // fenced (see the prologue).  Inputs are old means, fixed for the sweep.
+    {
+        using P = ArPart<R, true>;
+        constexpr int NPA = P::NPA, MC = P::MC, NB = 16;   // NB nodes' means per LDS stage (zb scratch)
+        const int Tt = dm.T_total, tg = dm.t_begin + t;
+        const bool act = tid < NPA * D;
+        const int k = act ? tid / NPA : 0, pp = tid % NPA;
+        const size_t DD = (size_t)D * D;
+        double c[MC];
+#pragma unroll
+        for (int mm = 0; mm < MC; ++mm) {
+            const int m = pp * MC + mm;
+            c[mm] = (m < D) ? a.consts[4 * DD + (size_t)k * D + m] : 0.0;
+        }
+        float* ms = (float*)zb;
+        double* outp = a.work + ame_v2_ring_doubles(&dm) + ((size_t)t * n + base) * (NPA * D);
+        const float* src = (tg >= Tt - 1) ? nullptr
+                         : (t < TL - 1) ? a.x_old + ((size_t)(t + 1) * n + base) * D
+                                        : a.next_old + (size_t)base * D;
+        for (int j0 = 0; j0 < cnt; j0 += NB) {
+            const int nb = min(NB, cnt - j0);
+            for (int e = tid; e < nb * D; e += AME_NT) ms[e] = src ? src[(size_t)j0 * D + e] : 0.f;
+            __syncthreads();
+            if (act) {
+                for (int qn = 0; qn < nb; ++qn) {
+                    const float* mr = ms + qn * D;
+                    double pR[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                    for (int mm = 0; mm < MC; ++mm) {
+                        const int m = pp * MC + mm;
+                        const float x = (m < D) ? mr[m] : 0.f;
+                        pR[mm & 3] = fma(c[mm], (double)x, pR[mm & 3]);
+                    }
+                    outp[(size_t)(j0 + qn) * (NPA * D) + tid] = (pR[0] + pR[1]) + (pR[2] + pR[3]);
+                }
+            }
+            __syncthreads();
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // before any partial store
+    }
     float mreg[AME_GW_MAXPW];
 #pragma unroll
     for (int s2 = 0; s2 < AME_GW_MAXPW; ++s2) {
@@ -562,7 +565,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
 
     const int at = WK ? tid - 64 : tid;   // AR thread index
     // AR rows: thread (k = at / NPA, part = at % NPA); WK reads the PhiTQi half
-    // precomputed (ame_ar_right_kernel)
+    // precomputed by the GEMV workers before the sweep loop
     // WK keeps QiPhi in LDS by row part (MCP: MC padded to even, 16-B rows)
     constexpr int MCP = (MC + 1) & ~1;
     double qiphi[WK ? 1 : MC], phitqi[WK ? 1 : MC];
@@ -787,7 +790,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         }
     };
     // WK: the PhiTQi mu_right half of node `node`, precomputed before the sweep
-    // (ame_ar_right_kernel; the work buffer past the partial ring); the QiPhi
+    // (by the GEMV workers; the work buffer past the partial ring); the QiPhi
     // mu_left half once wave 1 has polled mu_left
     const double* arr = WK ? a.work + ame_v2_ring_doubles(&dm) + (size_t)tl * n * (NPA * D) : nullptr;
     auto ar_right_load = [&](int node) -> double {
@@ -990,6 +993,9 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         else gemv(tid - 64);
     }
     __syncthreads();
+    // WK: every worker stored its nodes' right AR terms before its partial 0,
+    // which the gather above has seen: acquire them for the whole workgroup
+    if constexpr (WK) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     gemv_reduce(0);
     if constexpr (WK) ar_left_finish(0, ar_right_load(0));
     else ar_terms(0);
@@ -1327,7 +1333,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 STAMPW(8, 0);
                 M22 Mm = {Rm.a + o[0], Rm.b + 0.5 * (o[1] + o[2]), 0.0, Rm.d + o[3]};
                 Mm.c = Mm.b;
-                M22 Mi = inv22(Mm);
+                M22 Mi = inv22_fast(Mm);
                 Mi.b = Mi.c = 0.5 * (Mi.b + Mi.c);
                 // rows 0, 1 of W (J K[:,b] = (W0[b], W1[b])) live in lanes 0, 1 of h = 0
                 const double Wa00 = ame::lane_bcast(W0[0], 0), Wa01 = ame::lane_bcast(W0[0], 1);
@@ -1395,7 +1401,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 wave_multidot<4, D, KH>(pr2, o2, red, scal + 16, lane);
                 M22 Sm = {Rm.a - o2[0], Rm.b - 0.5 * (o2[1] + o2[2]), 0.0, Rm.d - o2[3]};
                 Sm.c = Sm.b;
-                M22 Si = inv22(Sm);
+                M22 Si = inv22_fast(Sm);
                 Si.b = Si.c = 0.5 * (Si.b + Si.c);
 #pragma unroll
                 for (int h = 0; h < KH; ++h) {
@@ -1410,9 +1416,11 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             for (int h = 0; h < KH; ++h) {
                 const int k = lane + 64 * h;
                 if (k < D) {
-                    upd[k] = Lp0[h]; upd[D + k] = Lp1[h]; upd[2 * D + k] = Rp0[h]; upd[3 * D + k] = Rp1[h];
-                    upd[4 * D + k] = Lm0[h]; upd[5 * D + k] = Lm1[h];
-                    upd[6 * D + k] = Rm0[h]; upd[7 * D + k] = Rm1[h];
+                    // row-interleaved: the k-side four of an entry, then its m-side
+                    // four, each one 32-byte run (two 16-byte LDS reads in phase 3)
+                    double* ur = upd + 8 * k;
+                    ur[0] = Lp0[h]; ur[1] = Lp1[h]; ur[2] = Lm0[h]; ur[3] = Lm1[h];
+                    ur[4] = Rp0[h]; ur[5] = Rp1[h]; ur[6] = Rm0[h]; ur[7] = Rm1[h];
                 }
             }
             if (is_naive) {
@@ -1478,7 +1486,9 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 P2STAMP(2 * (wave - 1));
                 if (lane == 0) ame::lds_signal_add(wave == 1 ? wsync + 1 : wsync, 1u);
                 ame::lds_wait_ge(wsync + 1, (uint32_t)(i + 1), a.status, dead);
+                P2STAMP(8 + 2 * (wave - 1));
                 ar_left_finish(i + 1, aR);
+                P2STAMP(9 + 2 * (wave - 1));
                 P2STAMP(6);
                 ame::lds_wait_ge(wsync, 2u * (uint32_t)(i + 1), a.status, dead);
                 gemv_reduce(i + 1);
@@ -1518,8 +1528,10 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 const int qq = q0 + b < LTQ ? q0 + b : LTQ - 1;
                 const int k = max(lk[qq], 0), m = max(lm[qq], 0);
                 kr[b] = K[k * KS + m];
-                u0[b] = upd[k]; u1[b] = upd[2 * D + m]; u2[b] = upd[D + k]; u3[b] = upd[3 * D + m];
-                u4[b] = upd[4 * D + k]; u5[b] = upd[6 * D + m]; u6[b] = upd[5 * D + k]; u7[b] = upd[7 * D + m];
+                const double* uk = upd + 8 * k;       // Lp0 Lp1 Lm0 Lm1 of row k
+                const double* um = upd + 8 * m + 4;   // Rp0 Rp1 Rm0 Rm1 of row m
+                u0[b] = uk[0]; u2[b] = uk[1]; u4[b] = uk[2]; u6[b] = uk[3];
+                u1[b] = um[0]; u3[b] = um[1]; u5[b] = um[2]; u7[b] = um[3];
                 ckm[b] = cob[k * D + m];
                 cmk[b] = cob[m * D + k];
                 nd[b] = ndiag[k];   // naive only (C = diag(1 / (diag(P_i) + 1e-8)), formed in phase 2)
@@ -1585,12 +1597,6 @@ static int launch_sweep_t(const ame_dims* dm, const ame_sweep_args* a, hipStream
         if (hipMemsetAsync(a->work, 0, bytes, st) != hipSuccess) return -3;
         static_assert(ArPart<R, true>::NPA == ((4 * (2 + 2 * R) <= 192) ? 4 : 2),
                       "ame_v2_arr_doubles sizes the AR parts");
-        const long long nb = (long long)dm->T_local * ((dm->n + AR_NB - 1) / AR_NB);
-        if (nb > 0) {
-            hipLaunchKernelGGL(ame_ar_right_kernel<R>, dim3((unsigned)nb), dim3(AME_NT), 0, st, *dm, *a,
-                               a->work + ame_v2_ring_doubles(dm));
-            if (hipGetLastError() != hipSuccess) return -3;
-        }
     }
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(AME_NT), (size_t)lds, st, *dm, *a);
     return hipGetLastError() == hipSuccess ? 0 : -3;

@@ -113,14 +113,16 @@ def run():
         print(f"    +{d:8.0f} after phase start: {sub[ph]}")
     if hasattr(L, "ame_debug_read_p2stamps"):   # phase 2 of waves 1-3 (kind 22)
         L.ame_debug_read_p2stamps.argtypes = [ctypes.c_void_p]
-        pb = (ctypes.c_ulonglong * (16 * 8))()
+        pb = (ctypes.c_ulonglong * (16 * 16))()
         if L.ame_debug_read_p2stamps(pb) == 0 and pb[0]:
             names = {0: "w1 signalled", 2: "w2 signalled", 4: "w3 signalled", 6: "AR-left done (last wave)",
-                     1: "w1 reduce+AR done", 3: "w2 reduce+AR done", 5: "w3 reduce+AR done"}
+                     1: "w1 reduce+AR done", 3: "w2 reduce+AR done", 5: "w3 reduce+AR done",
+                     8: "w1 AR-left start", 9: "w1 AR-left end", 10: "w2 AR-left start", 11: "w2 AR-left end",
+                     12: "w3 AR-left start", 13: "w3 AR-left end"}
             for sl in sorted(names):
-                d = sorted(pb[k * 8 + sl] - rows[k][1] for k in range(15))[7]
+                d = sorted(pb[k * 16 + sl] - rows[k][1] for k in range(15))[7]
                 print(f"    +{d:8d} after phase-2 start: {names[sl]}")
-            d = sorted(pb[k * 8 + 7] - rows[k][0] for k in range(15))[7]
+            d = sorted(pb[k * 16 + 7] - rows[k][0] for k in range(15))[7]
             print(f"    +{d:8d} after phase-1 start: w1 matvec items done")
     if hasattr(L, "ame_debug_read_wstamps"):   # GEMV worker 0 of the same slice (kind 22)
         L.ame_debug_read_wstamps.argtypes = [ctypes.c_void_p]
