@@ -28,4 +28,17 @@ def test_cov_exactly_symmetric(n, T, r, method, kind, gpu_device):
     vi.fit(max_iter=2, tolerance=0.0, verbose=False)
     C = vi.X_cov.numpy()
     asym = np.argwhere(C != np.swapaxes(C, -1, -2))
+    if len(asym):
+        # diagnostics for a recurrence (seen once in a full-suite run, not
+        # reproduced in 12 repetitions): magnitude, and whether the
+        # in-order schedule of the same fit agrees
+        m2 = TemporalAMEModel(n, T, r, seed=2)
+        m2.generate_data_fast(seed=3)
+        v2 = _vi(m2, method, 0.7, gpu_device, sweep_kernel=kind, pipeline=False, speculate=False)
+        v2.fit(max_iter=2, tolerance=0.0, verbose=False)
+        C2 = v2.X_cov.numpy()
+        print("asymmetric entries", len(asym), "max", np.abs(C - np.swapaxes(C, -1, -2)).max(),
+              "in-order run asymmetric", np.count_nonzero(C2 != np.swapaxes(C2, -1, -2)),
+              "max |C - C_inorder|", np.abs(C - C2).max(),
+              "max |mean - mean_inorder|", np.abs(vi.X_mean.numpy() - v2.X_mean.numpy()).max())
     assert len(asym) == 0, (len(asym), asym[:5].tolist())
