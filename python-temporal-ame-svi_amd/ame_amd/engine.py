@@ -311,6 +311,18 @@ class DeviceEngine:
             while len(self.xs) < self.spec_depth + 1:
                 self.xs.append(torch.empty_like(self.xs[0]))
                 self.covs.append(torch.empty_like(self.covs[0]))
+        self._host_ready = None
+        self._mark_host_writes()
+
+    def _mark_host_writes(self):
+        """Record the main-stream position after host-issued writes to the state
+        or the sweep's flags (uploads, zero fills, set_means / set_covs).  A
+        pipelined launch orders itself on the device against the previous sweep
+        only; this event orders it after these writes as well (its stream has no
+        other tie to the main stream)."""
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        self._host_ready = ev
 
     # current state (ring slot _cur)
     @property
@@ -395,6 +407,7 @@ class DeviceEngine:
         wait = 0
         if pipe:
             wait = self.epoch - 1
+            stream.wait_event(self._host_ready)
         else:
             ready = torch.cuda.Event()
             ready.record(self.stream)
@@ -426,6 +439,12 @@ class DeviceEngine:
             _lib.check(self.L.ame_sweep(ctypes.byref(dims), ctypes.byref(a),
                                         ctypes.c_void_p(stream.cuda_stream)), "ame_sweep")
         self._toc(tok)
+        # the kernels take raw pointers: tell the caching allocator this stream
+        # uses the buffers, so a dropped engine's memory is not handed out again
+        # while a sweep still reads or writes it
+        for t in (self.xs[src], self.xs[dst], self.covs[src], self.covs[dst], self.hand,
+                  self.done, self.status, self.sweep_work, self.Yt, self.consts):
+            t.record_stream(stream)
         done = torch.cuda.Event()
         done.record(stream)
         return done, dst
@@ -543,6 +562,7 @@ class DeviceEngine:
         sh = self.shard
         t0, t1 = sh.t_begin, sh.t_begin + sh.T_local
         self.x_a.copy_(X_mean[:, t0:t1].detach().float().permute(1, 0, 2))
+        self._mark_host_writes()
         self.invalidate()
 
     def set_covs(self, X_cov: torch.Tensor):
@@ -550,4 +570,5 @@ class DeviceEngine:
         sh = self.shard
         t0, t1 = sh.t_begin, sh.t_begin + sh.T_local
         self.cov.copy_(X_cov[:, t0:t1].detach().float().permute(1, 0, 2, 3))
+        self._mark_host_writes()
         self.invalidate()

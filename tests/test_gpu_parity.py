@@ -283,6 +283,49 @@ def test_unpipelined_queue_is_one_deep(gpu_device):
     assert [float(e) for e in ha["elbo"]] == [float(e) for e in hb["elbo"]]
 
 
+def test_pipelined_sweep_after_device_state_write(gpu_device):
+    """A pipelined sweep started right after the state was written on the main
+    stream (set_means from a device tensor, queued behind a long kernel) reads
+    the written state: its only device-side wait is on the previous sweep, so
+    the launch also waits for the host-issued writes (_mark_host_writes)."""
+    a, b = _twins(150, 20, 4, "good", 0.5, gpu_device)
+    assert a.engine.pipelined
+    for vi in (a, b):
+        vi.fit(max_iter=1, tolerance=0.0, verbose=False)
+    X = a.X_mean.clone()
+    X[:, :, 0] += 0.25
+    outs = []
+    for vi in (a, b):
+        eng = vi.engine
+        big = torch.randn(4096, 4096, device=gpu_device)
+        for _ in range(8):   # keep the main stream busy well past the launch
+            big = big @ big.T * 1e-3
+        eng.set_means(X.to(gpu_device))
+        eng.terms(speculate=1 if eng.speculation else 0)
+        eng.sweep()
+        eng.terms()
+        outs.append((eng.means_local().cpu().clone(), eng.covs_local().cpu().clone()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+def test_engine_dropped_with_sweep_queued(gpu_device):
+    """An engine dropped while a started sweep still runs: the sweep streams are
+    recorded on every buffer a launch passes as a raw pointer, so the caching
+    allocator does not hand that memory to the next engine early; the next fit of
+    the same shape is bit-identical to the in-order schedule."""
+    import gc
+    a, _ = _twins(150, 20, 4, "good", 0.5, gpu_device)
+    a.fit(max_iter=1, tolerance=0.0, verbose=False)
+    a.engine.speculate(1)
+    del a, _
+    gc.collect()
+    b, c = _twins(150, 20, 4, "good", 0.5, gpu_device)
+    b.fit(max_iter=2, tolerance=0.0, verbose=False)
+    c.fit(max_iter=2, tolerance=0.0, verbose=False)
+    assert np.array_equal(b.X_mean.numpy(), c.X_mean.numpy())
+    assert np.array_equal(b.X_cov.numpy(), c.X_cov.numpy())
+
+
 def test_state_attributes_stay_live(gpu_device):
     """X = vi.X_mean taken before fit() sees the fitted values once the
     attribute is read again (reference getters return the live tensor,
