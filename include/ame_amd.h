@@ -55,6 +55,10 @@ enum ame_variant { AME_GOOD = 0, AME_BAD = 1, AME_NAIVE = 2 };
 #define AME_STATUS_SPIN_TIMEOUT 1u
 #define AME_STATUS_HALO_TIMEOUT 2u
 #define AME_STATUS_LDS_TIMEOUT 4u   /* intra-workgroup hand-off timed out (internal error) */
+/* a hand-off word (done flag, back-channel done word, {epoch, value} granule)
+ * carried an epoch the protocol cannot have produced yet: a stale buffer or an
+ * unordered host write; the word is not consumed as if it were current */
+#define AME_STATUS_STALE_EPOCH 8u
 
 /* float offset of the done word in a back channel of n*d floats */
 #define AME_BACK_DONE_OFFSET(nd) ((((nd) + 63) / 64) * 64)

@@ -16,6 +16,7 @@ AME_GOOD, AME_BAD, AME_NAIVE = 0, 1, 2
 AME_STATUS_SPIN_TIMEOUT = 1
 AME_STATUS_HALO_TIMEOUT = 2
 AME_STATUS_LDS_TIMEOUT = 4
+AME_STATUS_STALE_EPOCH = 8
 AME_PEER_HANDLE_BYTES = 64
 # sweep kernel requests / kinds (enum ame_sweep_kind_code)
 AME_SWEEP_AUTO, AME_SWEEP_V2_SINGLE, AME_SWEEP_V2_AUTO, AME_SWEEP_V3 = 0, 1, 2, 3

@@ -308,9 +308,16 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
                 const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
                 while (true) {
                     __builtin_amdgcn_s_sleep(2);
+                    bool stale = false;
                     if (need) {
                         v = gran_load_agent(hand + (size_t)jn * D + 2 + lane);
                         ok = (uint32_t)(v >> 32) == a.epoch;
+                        stale = (uint32_t)(v >> 32) > a.epoch;   // no later sweep can have written it yet
+                    }
+                    if (__any(stale)) {
+                        if (lane == 0) atomicOr(a.status, AME_STATUS_STALE_EPOCH);
+                        dead = true;
+                        break;
                     }
                     if (__all(ok)) break;
                     if (__builtin_amdgcn_s_memrealtime() - t0 > AME_SPIN_TICKS_LOCAL) {
@@ -865,13 +872,20 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             while (true) {
                 __builtin_amdgcn_s_sleep(2);
                 ok = true;
+                bool stale = false;
 #pragma unroll
                 for (int h = 0; h < KH; ++h) {
                     const int k = lane + 64 * h;
                     if (k < D) {
                         v[h] = from_halo ? gran_load_system(src + k) : gran_load_agent(src + k);
                         ok = ok && (uint32_t)(v[h] >> 32) == a.epoch;
+                        stale = stale || (uint32_t)(v[h] >> 32) > a.epoch;   // see ame_sweep3.hip gran_finish
                     }
+                }
+                if (__any(stale)) {
+                    if (lane == 0) atomicOr(a.status, AME_STATUS_STALE_EPOCH);
+                    dead = true;
+                    break;
                 }
                 if (__all(ok)) break;
                 if (__builtin_amdgcn_s_memrealtime() - t_start > budget) {

@@ -263,9 +263,19 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             const uint64_t budget = (tl == 0) ? AME_SPIN_TICKS_HALO : AME_SPIN_TICKS_LOCAL;
             const uint64_t* src = gran_src(node);
             while (true) {
+                // a tag above this sweep's epoch cannot come from slice t-1 of
+                // this sweep or an earlier one (the next sweep's slice t-1 waits
+                // for this slice's done flag): stale memory, reported, not consumed
+                bool stale = false;
                 if (lane < D) {
                     v = (tl == 0) ? gran_load_system(src + lane) : gran_load_agent(src + lane);
                     ok = (uint32_t)(v >> 32) == a.epoch;
+                    stale = (uint32_t)(v >> 32) > a.epoch;
+                }
+                if (__any(stale)) {
+                    if (lane == 0) atomicOr(a.status, AME_STATUS_STALE_EPOCH);
+                    dead = true;
+                    break;
                 }
                 if (__all(ok)) break;
                 if (__builtin_amdgcn_s_memrealtime() - t0 > budget) {
@@ -337,9 +347,21 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     if (a.wait_epoch != 0u) {
         if (tid == 0) {
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            // Epoch window: while this sweep (wait_epoch + 1) waits, neither flag
+            // can exceed wait_epoch -- sweep wait_epoch + 1 writes done[t] only
+            // when it finishes slice t, the sweeps queued behind it wait for that,
+            // and slice t+1 cannot finish before slice t.  A larger value is stale
+            // memory (a recycled buffer, a host write not yet ordered before this
+            // launch): it sets AME_STATUS_STALE_EPOCH instead of being taken as done.
             for (int q = 0; q < 2 && tl + q < TL; ++q) {
-                while (__hip_atomic_load(a.done + tl + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-                       a.wait_epoch) {
+                while (true) {
+                    const uint32_t dv = __hip_atomic_load(a.done + tl + q, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+                    if (dv > a.wait_epoch) {
+                        atomicOr(a.status, AME_STATUS_STALE_EPOCH);
+                        break;
+                    }
+                    if (dv == a.wait_epoch) break;
                     if (__builtin_amdgcn_s_memrealtime() - t0 > AME_SPIN_TICKS_LOCAL) {
                         atomicOr(a.status, AME_STATUS_SPIN_TIMEOUT);
                         break;
@@ -349,8 +371,16 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             }
             if (back_rd) {   // the right rank's first slice of the previous sweep
                 const uint32_t* bd = (const uint32_t*)(a.back_in + AME_BACK_DONE_OFFSET(n * D));
-                while (__hip_atomic_load(const_cast<uint32_t*>(bd), __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_SYSTEM) < a.wait_epoch) {
+                while (true) {
+                    // same window: the right rank's first slice of THIS sweep
+                    // needs this slice's hand-off granules before it can finish
+                    const uint32_t dv = __hip_atomic_load(const_cast<uint32_t*>(bd), __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (dv > a.wait_epoch) {
+                        atomicOr(a.status, AME_STATUS_STALE_EPOCH);
+                        break;
+                    }
+                    if (dv == a.wait_epoch) break;
                     if (__builtin_amdgcn_s_memrealtime() - t0 > AME_SPIN_TICKS_HALO) {
                         atomicOr(a.status, AME_STATUS_HALO_TIMEOUT);
                         break;

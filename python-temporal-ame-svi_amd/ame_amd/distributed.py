@@ -74,13 +74,6 @@ class PeerBuffer:
             self.handle = handle
             self.owner = False
 
-    def quiesce_local(self, eng):
-        """Exception path of fit(): wait for this rank's own kernels only (no
-        collective: the other ranks may be inside a different one)."""
-        if self._peers is None:
-            return
-        torch.cuda.synchronize(eng.dev)
-
     def close(self):
         if self.dev is None or not self.dev.value:
             return
@@ -138,9 +131,19 @@ class TimeShardHalo:
             dist.all_gather_object(allh, mine, group=self.group)
             peer_halo = PeerBuffer(handle=allh[rank + 1][0]) if rank < world - 1 else None
             peer_back = PeerBuffer(handle=allh[rank - 1][1]) if rank > 0 else None
-        self._peers = (own_halo, own_back, peer_halo, peer_back)
+        peers = (own_halo, own_back, peer_halo, peer_back)
+        try:
+            self._preflight(eng, peers)
+        except Exception:
+            # nothing may sweep over a link that failed: _peers stays unset, so a
+            # caller that catches this and fits again re-runs the setup (and the
+            # pre-flight) instead of spinning on the bad link
+            for p in peers:
+                if p is not None:
+                    p.close()
+            raise
+        self._peers = peers
         atexit.register(self.close)
-        self._preflight(eng)
 
     @staticmethod
     def _sentinel(kind: int, writer: int, owner: int) -> int:
@@ -148,7 +151,7 @@ class TimeShardHalo:
         # up from 1), and the buffers are zeroed again after the check
         return ((0xA3E50000 | (kind << 12) | (writer & 0xFFF)) << 32) | (owner & 0xFFFFFFFF)
 
-    def _preflight(self, eng, wait_s: float = 2.0):
+    def _preflight(self, eng, peers, wait_s: float = 2.0):
         """Every peer link once, before the first sweep: each rank stores a
         sentinel into each buffer it MAPPED (the right neighbour's halo, the left
         neighbour's back channel) with the same system-scope store the sweep's
@@ -160,16 +163,28 @@ class TimeShardHalo:
         import time
         L = _lib.lib()
         rank = self.shard.rank
-        own_halo, own_back, peer_halo, peer_back = self._peers
+        own_halo, own_back, peer_halo, peer_back = peers
+        bad = []
+
+        def call(fn, *args, what):
+            # a library error is recorded, never raised here: every rank must
+            # reach the barrier and the all_reduce below, or its peers would wait
+            # in them until the process-group timeout
+            try:
+                _lib.check(fn(*args), what)
+                return True
+            except Exception as e:   # noqa: BLE001 -- reported on every rank below
+                bad.append(f"rank {rank}: {e}")
+                return False
+
         with torch.cuda.device(eng.dev):
             if peer_halo is not None:
-                _lib.check(L.ame_peer_probe(peer_halo.dev, self._sentinel(1, rank, rank + 1)),
-                           f"ame_peer_probe (rank {rank} -> halo of rank {rank + 1})")
+                call(L.ame_peer_probe, peer_halo.dev, self._sentinel(1, rank, rank + 1),
+                     what=f"ame_peer_probe (rank {rank} -> halo of rank {rank + 1})")
             if peer_back is not None:
-                _lib.check(L.ame_peer_probe(peer_back.dev, self._sentinel(2, rank, rank - 1)),
-                           f"ame_peer_probe (rank {rank} -> back channel of rank {rank - 1})")
+                call(L.ame_peer_probe, peer_back.dev, self._sentinel(2, rank, rank - 1),
+                     what=f"ame_peer_probe (rank {rank} -> back channel of rank {rank - 1})")
         dist.barrier(group=self.group)
-        bad = []
         with torch.cuda.device(eng.dev):
             for buf, writer, kind, nbytes, what in (
                     (own_halo, rank - 1, 1, eng.n * eng.d * 8, "left halo"),
@@ -179,15 +194,19 @@ class TimeShardHalo:
                 want = self._sentinel(kind, writer, rank)
                 got = ctypes.c_ulonglong(0)
                 t0 = time.monotonic()
+                read_ok = True
                 while True:
-                    _lib.check(L.ame_peer_read_u64(buf.dev, ctypes.byref(got)), "ame_peer_read_u64")
+                    if not call(L.ame_peer_read_u64, buf.dev, ctypes.byref(got),
+                                what=f"ame_peer_read_u64 ({what} of rank {rank})"):
+                        read_ok = False
+                        break
                     if got.value == want or time.monotonic() - t0 > wait_s:
                         break
                     time.sleep(0.01)
-                if got.value != want:
+                if read_ok and got.value != want:
                     bad.append(f"rank {writer} -> rank {rank} ({what}): read {got.value:#018x}, "
                                f"expected {want:#018x}")
-                _lib.check(L.ame_peer_clear(buf.dev, nbytes), "ame_peer_clear")
+                call(L.ame_peer_clear, buf.dev, nbytes, what=f"ame_peer_clear ({what} of rank {rank})")
         flag = torch.tensor([len(bad)], dtype=torch.int32,
                             device="cpu" if self._host_coll else eng.dev)
         dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
@@ -231,7 +250,21 @@ class TimeShardHalo:
         dist.all_gather(out, src, group=self.group)
         return [o.to(t.device) for o in out]
 
+    def quiesce_local(self, eng):
+        """Exception path of fit(): wait for this rank's own kernels only (no
+        collective: the other ranks may be inside a different one)."""
+        if self._peers is None:
+            return
+        torch.cuda.synchronize(eng.dev)
+
     # ---- engine hooks ----
+    def agree_max(self, eng, value: int) -> int:
+        """The maximum of `value` over all ranks (the engines' epoch base)."""
+        t = torch.tensor([int(value)], dtype=torch.int64,
+                         device="cpu" if self._host_coll else eng.dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return int(t.item())
+
     def agree(self, eng, flag: bool) -> bool:
         """True only if every rank passes True."""
         t = torch.tensor([1 if flag else 0], dtype=torch.int32,

@@ -119,6 +119,39 @@ def derive_spec_depth(n: int, T_total: int) -> int:
     return max(2, min(MAX_SPEC_DEPTH, need))
 
 
+# Sweep epochs are unique within the process: every engine starts above the
+# highest epoch any earlier engine launched.  A buffer the caching allocator
+# recycles from an older engine (done flags, hand-off granules) then only
+# holds epochs BELOW every epoch this engine waits for, so a stale word makes
+# a waiter wait instead of passing; the device additionally flags any word
+# ABOVE the epoch window (AME_STATUS_STALE_EPOCH, include/ame_amd.h).
+_EPOCH_HIGH = 0
+
+
+def _epoch_base() -> int:
+    return _EPOCH_HIGH
+
+
+def _note_epoch(e: int) -> None:
+    global _EPOCH_HIGH
+    _EPOCH_HIGH = max(_EPOCH_HIGH, int(e))
+
+
+_STATUS_TEXT = (
+    (_lib.AME_STATUS_SPIN_TIMEOUT, "a hand-off between slices timed out (workgroups not co-resident?)"),
+    (_lib.AME_STATUS_HALO_TIMEOUT, "a hand-off from a neighbouring rank timed out"),
+    (_lib.AME_STATUS_LDS_TIMEOUT, "an intra-workgroup hand-off timed out (internal error)"),
+    (_lib.AME_STATUS_STALE_EPOCH, "a hand-off word carried an epoch outside the protocol's "
+                                  "window (stale buffer or an unordered write): results of "
+                                  "this sweep are not trusted"),
+)
+
+
+def status_text(st: int) -> str:
+    parts = [txt for bit, txt in _STATUS_TEXT if st & bit]
+    return "; ".join(parts) if parts else "unknown"
+
+
 def _ptr(t: Optional[torch.Tensor]):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
@@ -249,7 +282,9 @@ class DeviceEngine:
             self.work = torch.empty(ws, dtype=torch.float64, device=dev)
             self.out = torch.zeros(8, dtype=torch.float64, device=dev)
             self.status = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.epoch = 0
+        self.epoch = _epoch_base()
+        if self.halo is not None:   # every rank's sweep k carries the same epoch
+            self.epoch = self.halo.agree_max(self, self.epoch)
         self.max_slices = int(self.L.ame_sweep_max_slices(self.n, self.r, opt.sweep_kernel))
         if self.max_slices < 1:
             raise RuntimeError(f"ame_amd: no sweep kernel fits n={self.n}, r={self.r} "
@@ -312,6 +347,10 @@ class DeviceEngine:
                 self.xs.append(torch.empty_like(self.xs[0]))
                 self.covs.append(torch.empty_like(self.covs[0]))
         self._host_ready = None
+        # test hook only (tests/test_gpu_stale_epoch.py): False lets a pipelined
+        # launch skip the wait for host-issued writes, to show the device's
+        # epoch-window check catching the resulting stale flags
+        self._order_after_host_writes = True
         self._mark_host_writes()
 
     def _mark_host_writes(self):
@@ -391,6 +430,7 @@ class DeviceEngine:
         src = self._specs[-1][1] if self._specs else self._cur
         dst = (src + 1) % len(self.xs)
         self.epoch += 1
+        _note_epoch(self.epoch)
         # two streams: sweep k+2 queues behind sweep k's local slices, which keeps
         # the launch-order XCD placement of its workgroups (three streams, measured:
         # 16 % slower per iteration at n=128); the host-side constraint a deeper
@@ -407,7 +447,8 @@ class DeviceEngine:
         wait = 0
         if pipe:
             wait = self.epoch - 1
-            stream.wait_event(self._host_ready)
+            if self._order_after_host_writes:
+                stream.wait_event(self._host_ready)
         else:
             ready = torch.cuda.Event()
             ready.record(self.stream)
@@ -541,8 +582,11 @@ class DeviceEngine:
         st = int(self.status.item())
         if st:
             self.status.zero_()
-            raise RuntimeError(f"ame_amd: sweep reported device status {st:#x} "
-                               "(hand-off spin timed out: lanes not co-resident?)")
+            # a later pipelined launch must not start before this zero lands (it
+            # would erase that sweep's own status bits)
+            self._mark_host_writes()
+            raise RuntimeError(f"ame_amd: sweep reported device status {st:#x}: "
+                               f"{status_text(st)}")
 
     def invalidate(self):
         self._out_valid = False

@@ -140,12 +140,37 @@ def _preflight_worker(rank, world, port, q):
                                                               owner + 7 if kind == 1 else owner)
         msg = None
         try:
-            halo._preflight(vi.engine)
+            halo._preflight(vi.engine, halo._peers)
         except RuntimeError as e:
             msg = str(e)
         # the buffers were zeroed after the check: the sweep still runs
         vi.fit(max_iter=1, tolerance=0.0, verbose=False)
-        q.put((rank, msg))
+        if rank == 0:
+            halo._sentinel = real
+        # a library error inside the pre-flight (ame_peer_probe fails on rank 1):
+        # it must not raise before rank 1 reaches the barrier and the all_reduce,
+        # so both ranks raise and neither waits for the process-group timeout
+        from ame_amd import distributed as D
+        real_lib = D._lib.lib
+
+        class _FailProbe:
+            def __init__(self, L):
+                self._L = L
+
+            def __getattr__(self, name):
+                if name == "ame_peer_probe":
+                    return lambda *a: -1
+                return getattr(self._L, name)
+
+        if rank == 1:
+            D._lib.lib = lambda: _FailProbe(real_lib())
+        msg2 = None
+        try:
+            halo._preflight(vi.engine, halo._peers)
+        except RuntimeError as e:
+            msg2 = str(e)
+        D._lib.lib = real_lib
+        q.put((rank, msg, msg2))
     finally:
         dist.destroy_process_group()
 
@@ -153,7 +178,9 @@ def _preflight_worker(rank, world, port, q):
 def test_preflight_detects_bad_link():
     """The setup pre-flight of the peer links (distributed.py _preflight) raises
     on both ranks, naming the failing pair on its owner, when the word that
-    arrives is not the sentinel that was sent."""
+    arrives is not the sentinel that was sent -- and when a library call of the
+    pre-flight itself fails on one rank (both ranks still reach the collective,
+    so neither hangs)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     ctx = mp.get_context("spawn")
@@ -162,11 +189,12 @@ def test_preflight_detects_bad_link():
     procs = [ctx.Process(target=_preflight_worker, args=(rk, 2, port, q)) for rk in range(2)]
     for p in procs:
         p.start()
-    got = {}
+    got, got2 = {}, {}
     try:
         for _ in range(2):
-            rank, msg = q.get(timeout=150)
+            rank, msg, msg2 = q.get(timeout=150)
             got[rank] = msg
+            got2[rank] = msg2
     finally:
         for p in procs:
             p.join(timeout=30)
@@ -176,3 +204,6 @@ def test_preflight_detects_bad_link():
     assert [p.exitcode for p in procs] == [0, 0]
     assert got[1] is not None and "rank 0 -> rank 1 (left halo)" in got[1], got[1]
     assert got[0] is not None and "another rank" in got[0], got[0]
+    # the failing probe: rank 1 names the call, rank 0 sees its back channel empty
+    assert got2[1] is not None and "ame_peer_probe" in got2[1], got2[1]
+    assert got2[0] is not None and "rank 1 -> rank 0 (back channel)" in got2[0], got2[0]
