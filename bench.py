@@ -288,6 +288,61 @@ def secondary_config5(dev, steps=8, warmup=2):
         return {"error": f"{type(e).__name__}: {e}"}
 
 
+def sweep_alg_bytes(n, TL, d):
+    return kernel_bytes(n, TL, d)["sweep"]
+
+
+def config5_full(dev, steps=3, warmup=1, variants=("naive", "good", "bad")):
+    """BASELINE config 5's own workload on ONE GPU: n=4096, T=256, r=32 (d=66),
+    Naive-MF vs SMF-good vs SMF-bad on the same synthetic Y
+    (experiments/three_way_conparison.py:141-179).  The GEMV-worker sweep
+    (kind 22) runs as 8 consecutive slice groups of 32 per iteration.  Per
+    variant: `warmup` untimed fit() iterations, then `steps` timed ones
+    (synchronize on both sides) with HIP events around every kernel launch."""
+    from ame_amd import TemporalAMEModel, TemporalAMENaiveMFVI, TemporalAMEStructuredMFVI
+    n, T, r = 4096, 256, 32
+    d = 2 + 2 * r
+    m = TemporalAMEModel(n, T, r, seed=42)
+    m.generate_data_fast(device=dev)
+    units = T * n * (n - 1) / 2.0
+    out = {"metric": "config 5 three-way fit() iteration time", "unit": "ms/iteration",
+           "config": {"workload": "BASELINE config 5 on one GPU: n_nodes=4096, n_time=256, "
+                                  "latent_dim=32 (d=66), Naive-MF / SMF-good / SMF-bad on one Y, "
+                                  "lr=0.01", "n_nodes": n, "n_time": T, "latent_dim": r},
+           "steps": steps, "warmup": warmup, "data": "synthetic", "dtype": "f32", "variants": {}}
+    for method in variants:
+        if method == "naive":
+            vi = TemporalAMENaiveMFVI(m, learning_rate=0.01, device=dev)
+        else:
+            vi = TemporalAMEStructuredMFVI(m, factorization=method, learning_rate=0.01, device=dev)
+        eng = vi.engine
+        vi.fit(max_iter=warmup, tolerance=0.0, verbose=False)
+        eng.timing = True
+        eng.events.clear()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        h = vi.fit(max_iter=steps, tolerance=0.0, verbose=False)
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        kms, kcount = eng.kernel_ms()
+        ms = dt / steps * 1e3
+        alg = sweep_alg_bytes(n, T, d)
+        out["variants"][method] = {
+            "ms_per_iteration": ms, "updates_per_s": units / (ms * 1e-3),
+            "sweep_kind": int(eng.sweep_kind), "slice_groups": len(eng.groups),
+            "pipelined": bool(eng.pipelined),
+            "kernel_ms": kms, "kernel_launches": kcount,
+            "sweep_roofline": {"alg_bytes": alg, "ms": kms.get("sweep"),
+                               "frac": (alg / (kms["sweep"] * 1e-3) / 1e9 / HBM_PEAK_GBS)
+                               if kms.get("sweep") else None,
+                               "note": "algorithmic bytes of one full sweep (8 slice-group "
+                                       "launches) / its HIP-event time"},
+            "elbo_last": float(h["elbo"][-1]), "mse_last": float(h["reconstruction_error"][-1])}
+        del vi, eng
+        torch.cuda.empty_cache()
+    return out
+
+
 def main():
     # stdout carries exactly one JSON line: anything a library prints there
     # (RCCL's version banner at communicator creation, ...) goes to stderr
@@ -314,6 +369,9 @@ def main():
     ap.add_argument("--force-dist", action="store_true",
                     help="use the process group (nccl) and the time-sharded path even at world size 1 "
                          "(checks RCCL initialisation on a one-GPU box)")
+    ap.add_argument("--config5-full", action="store_true",
+                    help="BASELINE config 5's own workload (n=4096, T=256, r=32) three-way on "
+                         "this one GPU; prints its own JSON line instead of the metric")
     args = ap.parse_args()
 
     import torch.distributed as dist
@@ -327,6 +385,11 @@ def main():
     dev = torch.device("cuda", local_rank % max(ndev, 1))
     torch.cuda.set_device(dev)
     use_dist = world > 1 or args.force_dist
+    if args.config5_full:
+        out = config5_full(dev, steps=args.steps if args.steps != 50 else 3,
+                           warmup=args.warmup if args.warmup != 3 else 1)
+        print(json.dumps(out), file=json_out, flush=True)
+        return out
     if use_dist:
         dist.init_process_group("nccl", device_id=dev)
 

@@ -289,6 +289,19 @@ class DeviceEngine:
         if self.max_slices < 1:
             raise RuntimeError(f"ame_amd: no sweep kernel fits n={self.n}, r={self.r} "
                                f"(request {opt.sweep_kernel})")
+        req = opt.sweep_kernel
+        if req in (_lib.AME_SWEEP_AUTO, _lib.AME_SWEEP_V2_AUTO) and (
+                req == _lib.AME_SWEEP_V2_AUTO
+                or int(self.L.ame_sweep_max_slices(self.n, self.r, _lib.AME_SWEEP_V3)) < 1):
+            # beyond v3's reach the GEMV-worker sweep (kind 22) in slice groups of
+            # what co-resides beats ONE launch of the single-workgroup sweep over
+            # all slices: config 5 at T = 256 on one GPU, 8 groups of 32 vs kind 21
+            # (DESIGN.md §4 K1c); AUTO already picks kind 22 whenever T_local fits
+            w = int(self.L.ame_sweep_max_slices(self.n, self.r, _lib.AME_SWEEP_V2_WORKERS))
+            if 1 <= w < min(sh.T_local, self.max_slices):
+                gd = _lib.ame_dims(self.n, self.r, w, sh.t_begin, sh.T_total, self.vcode)
+                if int(self.L.ame_sweep_kind(ctypes.byref(gd), req)) == _lib.AME_SWEEP_V2_WORKERS:
+                    self.max_slices = w
         self.groups = slice_groups(sh.T_local, self.max_slices, opt.slice_group)
         # the kernel of each group size is resolved ONCE here and passed with
         # every launch (ame_sweep rejects a launch whose buffers were sized for
