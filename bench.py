@@ -84,10 +84,12 @@ def cpu_baseline(model, vi, n, T, d, budget_s=40.0):
     (SURVEY.md §8d), timed after the GPU's timed region:
 
     * main value: the vectorised numpy oracle in its statistics form
-      (oracle/ame_oracle.py sweep_stats + elbo_recon_fast, fp64, BLAS threads as
-      numpy uses them): ONE FULL ITERATION measured, not extrapolated, when the
-      sweep's estimate fits `budget_s` (config 3: it does); otherwise the sweep
-      is timed on a node prefix and extrapolated (said in `sample`);
+      (oracle/ame_oracle.py sweep_stats + elbo_recon_fast) in fp32, the
+      reference's dtype, BLAS threads as numpy uses them: ONE FULL ITERATION
+      measured, not extrapolated, when the sweep's estimate fits `budget_s`
+      (config 3: it does); otherwise the sweep is timed on a node prefix and
+      extrapolated (said in `sample`); the same in fp64 (the parity oracle)
+      beside it as ``fp64_statistics_form``;
     * ``direct_restatement``: the per-step restatement (update_node: P_obs / h_obs
       summed over all other nodes at every step, as the reference does) on a
       node sample, extrapolated; plus its committed full-iteration figures
@@ -111,26 +113,37 @@ def cpu_baseline(model, vi, n, T, d, budget_s=40.0):
     params = {k: getattr(model, k).detach().cpu().numpy().astype(np.float32)
               for k in ("R", "R_inv", "Sigma", "Psi", "Phi", "Q")}
     units = T * n * (n - 1) / 2.0
-    # --- statistics-form oracle: one full iteration ---
-    Xm, Xc = X32.astype(np.float64), C32.astype(np.float64)
-    k0 = min(n, 16)
-    t0 = time.perf_counter()
-    O.sweep_stats(Y, Xm, Xc, params, "good", 0.01, nodes=range(k0))
-    t_head = time.perf_counter() - t0
-    est = t_head / k0 * n
-    if k0 < n and est <= budget_s:
+
+    def stats_iteration(dt):
+        """One iteration of the statistics-form oracle in dtype dt: the full
+        sweep when its estimate fits the budget (else a node prefix,
+        extrapolated), then the ELBO / MSE."""
+        Xm, Xc = X32.astype(dt), C32.astype(dt)
+        k0 = min(n, 16)
         t0 = time.perf_counter()
-        O.sweep_stats(Y, Xm, Xc, params, "good", 0.01, nodes=range(k0, n))
-        t_sweep = t_head + time.perf_counter() - t0
-        swept = n
-    else:
-        t_sweep, swept = est, k0
-    mT = T if n * n * T <= (1 << 28) else max(1, (1 << 28) // (n * n))
-    t0 = time.perf_counter()
-    O.elbo_recon_fast(Y[:, :, :mT], Xm[:, :mT], Xc[:, :mT], params, "good")
-    t_elbo = (time.perf_counter() - t0) * T / mT
+        O.sweep_stats(Y, Xm, Xc, params, "good", 0.01, nodes=range(k0))
+        t_head = time.perf_counter() - t0
+        est = t_head / k0 * n
+        if k0 < n and est <= budget_s:
+            t0 = time.perf_counter()
+            O.sweep_stats(Y, Xm, Xc, params, "good", 0.01, nodes=range(k0, n))
+            t_sw = t_head + time.perf_counter() - t0
+            sw = n
+        else:
+            t_sw, sw = est, k0
+        mT = T if n * n * T <= (1 << 28) else max(1, (1 << 28) // (n * n))
+        t0 = time.perf_counter()
+        O.elbo_recon_fast(Y[:, :, :mT], Xm[:, :mT], Xc[:, :mT], params, "good", dtype=dt)
+        t_el = (time.perf_counter() - t0) * T / mT
+        return t_sw, sw, t_el, mT
+
+    # --- statistics-form oracle: one full iteration, fp32 (the reference's
+    # dtype) as the value, fp64 (the parity oracle) beside it ---
+    t_sweep, swept, t_elbo, mT = stats_iteration(np.float32)
     it_s = t_sweep + t_elbo
     full = swept == n and mT == T
+    t_sweep64, swept64, t_elbo64, mT64 = stats_iteration(np.float64)
+    it64 = t_sweep64 + t_elbo64
     # --- direct restatement: a node sample of the sweep, extrapolated ---
     Xd, Cd = X32.copy(), C32.copy()
     consts = O.prior_terms(params, T, np.float32)
@@ -174,9 +187,14 @@ def cpu_baseline(model, vi, n, T, d, budget_s=40.0):
         "value": units / it_s, "unit": UNIT, "cores": int(threads), "kind": "port",
         "full_iteration": full, "s_per_iteration": it_s,
         "sample": (f"numpy oracle, statistics form (oracle/ame_oracle.py sweep_stats + "
-                   f"elbo_recon_fast), fp64, {threads} BLAS threads: {how}; sweep {t_sweep:.1f} s "
+                   f"elbo_recon_fast), fp32, {threads} BLAS threads: {how}; sweep {t_sweep:.1f} s "
                    f"+ ELBO / MSE {t_elbo:.1f} s = {it_s:.1f} s per iteration"),
         **_host_info(),
+        "fp64_statistics_form": {
+            "value": units / it64, "unit": UNIT, "cores": int(threads), "kind": "port",
+            "s_per_iteration": it64, "full_iteration": swept64 == n and mT64 == T,
+            "sample": f"the same in fp64 (the parity oracle): sweep {t_sweep64:.1f} s + ELBO / MSE "
+                      f"{t_elbo64:.1f} s"},
         "direct_restatement": {
             "value": units / direct_it, "unit": UNIT, "cores": int(threads), "kind": "port",
             "sample": (f"oracle/ame_oracle.py update_node (P_obs / h_obs re-summed over all "
@@ -233,24 +251,30 @@ def load_pmc(tag):
     return None
 
 
-def scaling_model(n, T_total, world, depth, pipelined):
+# node steps of wavefront lag per slice of the in-order GEMV-worker sweep (kind
+# 22): profiles/r05_*_c5_fill.jsonl (iteration time at T_local = 32 vs 1)
+FILL_STEPS_KIND22 = 3.0
+
+
+def scaling_model(n, T_total, world, depth, pipelined, fill=None):
     """DESIGN.md §5 queue-depth model: node steps per iteration at this world
     size, against one GPU's n (predicted weak-scaling efficiency = n / that).
     Pipelined: max(n + hop, (F (T_total - 1) + n + delta) / (1 + depth));
     in order: the fill F (T_total - 1) + n every iteration."""
     sys.path.insert(0, os.path.join(ROOT, "python-temporal-ame-svi_amd"))
     from ame_amd.engine import ELBO_READ_STEPS, FILL_STEPS_PER_SLICE
+    F = FILL_STEPS_PER_SLICE if fill is None else fill
     hop = world - 1          # about one node step per rank boundary
-    fill = FILL_STEPS_PER_SLICE * (T_total - 1)
+    fill_steps = F * (T_total - 1)
     if pipelined:
-        steps = max(n + hop, (fill + n + ELBO_READ_STEPS) / (1 + depth))
-        one = max(n, (FILL_STEPS_PER_SLICE * (T_total // world - 1) + n + ELBO_READ_STEPS) / (1 + depth))
+        steps = max(n + hop, (fill_steps + n + ELBO_READ_STEPS) / (1 + depth))
+        one = max(n, (F * (T_total // world - 1) + n + ELBO_READ_STEPS) / (1 + depth))
     else:
-        steps = fill + n
-        one = FILL_STEPS_PER_SLICE * (T_total // world - 1) + n
+        steps = fill_steps + n
+        one = F * (T_total // world - 1) + n
     return {"node_steps_per_iteration": steps, "one_gpu_node_steps": one,
             "predicted_efficiency_vs_1gpu": one / steps, "spec_depth": depth,
-            "fill_steps_per_slice": FILL_STEPS_PER_SLICE}
+            "fill_steps_per_slice": F}
 
 
 def _lib_provenance():
@@ -265,25 +289,71 @@ def secondary_config5(dev, steps=8, warmup=2):
     """BASELINE config 5's per-rank shape (n=4096, T_local=32, r=32, SMF-good,
     lr 0.01; the GEMV-worker sweep) on the same GPU after the main measurement,
     so the driver's record carries the largest configuration too.  Reported
-    beside the metric, never as it."""
+    beside the metric, never as it.  Carries its own roofline (the sweep's
+    algorithmic bytes per iteration, PMC traffic from the committed pass),
+    per-kernel HIP-event times and the queue-depth scaling model at N = 8
+    (T_total = 256)."""
     from ame_amd import TemporalAMEModel, TemporalAMEStructuredMFVI
     try:
+        n, TL, r = 4096, 32, 32
+        d = 2 + 2 * r
         # the config-3 state stays resident (≈ 3 GB beside config 5's ≈ 9 GB)
-        m5 = TemporalAMEModel(4096, 32, 32, seed=42)
+        m5 = TemporalAMEModel(n, TL, r, seed=42)
         m5.generate_data_fast(device=dev)
         v5 = TemporalAMEStructuredMFVI(m5, factorization="good", learning_rate=0.01, device=dev)
         v5.fit(max_iter=warmup, tolerance=0.0, verbose=False)
+        eng = v5.engine
+        eng.timing = True
+        eng.events.clear()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         v5.fit(max_iter=steps, tolerance=0.0, verbose=False)
         torch.cuda.synchronize(dev)
         dt = time.perf_counter() - t0
+        kms, _ = eng.kernel_ms()
+        iso = isolated_ms(eng)
         ms = dt / steps * 1e3
-        units = 32 * 4096 * 4095 / 2.0
+        units = TL * n * (n - 1) / 2.0
+        kb = kernel_bytes(n, TL, d, eng.swap_consistent)
+        pmc_all = load_pmc(f"n{n}_T{TL}_r{r}_good") or {}
+        pmc = pmc_all.get("kernels", {})
+        kernels = {}
+        for name, kms_v, how in (
+                ("sweep", ms, "per-iteration time (in-order sweeps: one per iteration)"),
+                ("cov", iso.get("cov"), "isolated launch, HIP events on its stream"),
+                ("elbo", iso.get("elbo"), "isolated launch (pair + node + final kernels)"),
+                ("pairs", iso.get("pairs"), "the ELBO pair kernel alone, isolated launch")):
+            ent = {"alg_bytes": kb[name], "ms": kms_v, "timing": how,
+                   "launch_ms_in_fit": kms.get(name)}
+            if kms_v:
+                ach = kb[name] / (kms_v * 1e-3) / 1e9
+                ent.update(achieved_GBs=ach, frac=ach / HBM_PEAK_GBS)
+            pk = pmc.get({"elbo": "pairs"}.get(name, name))
+            if pk and pk.get("hbm_bytes_per_launch"):
+                ent["traffic"] = pk["hbm_bytes_per_launch"]
+                ent["traffic_over_alg"] = pk["hbm_bytes_per_launch"] / pk.get("alg_bytes", kb[name])
+                ent["traffic_source"] = pmc_all.get("_file")
+            kernels[name] = ent
+        sw = kernels["sweep"]
+        if kms.get("sweep"):
+            sw["frac_per_launch"] = kb["sweep"] / (kms["sweep"] * 1e-3) / 1e9 / HBM_PEAK_GBS
+        pipelined = bool(eng.pipelined)
+        depth = int(getattr(eng, "spec_depth", 1))
         return {"config": "BASELINE config 5 per-rank shape: n_nodes=4096, n_time=32, latent_dim=32 "
                           "(d=66), SMF-good fit iteration, lr=0.01, one GPU",
                 "ms_per_step": ms, "value": units / (ms * 1e-3), "unit": UNIT, "steps": steps,
-                "warmup": warmup, "sweep_kind": int(v5.engine.sweep_kind)}
+                "warmup": warmup, "sweep_kind": int(eng.sweep_kind), "pipelined": pipelined,
+                "roofline": {"bound": "hbm", "kernel": "sweep", "achieved": sw.get("achieved_GBs"),
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": sw.get("frac"),
+                             "traffic": sw.get("traffic"),
+                             "traffic_over_alg": sw.get("traffic_over_alg"),
+                             "note": "achieved = the sweep's algorithmic bytes per launch / "
+                                     "ms_per_step; traffic from the committed PMC pass"},
+                "kernels": kernels,
+                "scaling_model": scaling_model(n, TL * 8, 8, depth, pipelined,
+                                               fill=FILL_STEPS_KIND22 if not pipelined else None),
+                "scaling_model_note": "config 5 time-sharded over 8 GPUs (T_total = 256): "
+                                      "node steps per iteration at N = 8 vs one rank's 32 slices"}
     except Exception as e:   # never costs the main line
         return {"error": f"{type(e).__name__}: {e}"}
 

@@ -205,7 +205,7 @@ def _slice_stats(M, r):
     Returns [count, sU, sV, S_UU, S_VV, S_VU] with S_VU = sum_j V_j U_j^T."""
     U, V = M[:, :, :r], M[:, :, r:]
     Ut, Vt = np.swapaxes(U, 1, 2), np.swapaxes(V, 1, 2)
-    return [np.full(M.shape[0], float(M.shape[1])), U.sum(1), V.sum(1),
+    return [np.full(M.shape[0], float(M.shape[1]), dtype=M.dtype), U.sum(1), V.sum(1),
             np.matmul(Ut, U), np.matmul(Vt, V), np.matmul(Vt, U)]
 
 
@@ -218,7 +218,7 @@ def _p_obs(st, R_inv, r):
     d = 2 + 2 * r
     p, q, q2, s = R_inv[0, 0], R_inv[0, 1], R_inv[1, 0], R_inv[1, 1]
     A, B, Ub, Vb = 0, 1, slice(2, 2 + r), slice(2 + r, d)
-    P = np.zeros((T, d, d))
+    P = np.zeros((T, d, d), dtype=sU.dtype)
     P[:, A, A] = p * m
     P[:, A, Ub] = p * sV
     P[:, Ub, A] = p * sV
@@ -247,17 +247,19 @@ def sweep_stats(Y, X_mean, X_cov, params, variant, lr, nodes=None):
     its inverse, the right AR term); only mu_{i,t} = C_t (h_t + Q^-1 Phi
     mu_{i,t-1}) runs as a loop.  Pinned to :func:`sweep` in
     tests/test_oracle_fast.py; used where the direct restatement is too slow
-    (full sweeps at n = 1024-4096)."""
+    (full sweeps at n = 1024-4096).  The arithmetic dtype is X_mean's: fp64 is
+    the parity oracle; fp32 (the reference's dtype) only times the CPU baseline
+    of bench.py."""
     n, T, d = X_mean.shape
     r = (d - 2) // 2
-    assert X_mean.dtype == np.float64 and X_cov.dtype == np.float64
-    R_inv = params["R_inv"].astype(np.float64)
-    Q_inv, S0_inv, PtQiP = prior_terms({k: v.astype(np.float64) for k, v in params.items()},
-                                       T, np.float64)
-    Phi = params["Phi"].astype(np.float64)
+    dt = X_mean.dtype
+    assert dt in (np.float64, np.float32) and X_cov.dtype == dt
+    R_inv = params["R_inv"].astype(dt)
+    Q_inv, S0_inv, PtQiP = prior_terms({k: v.astype(dt) for k, v in params.items()}, T, dt)
+    Phi = params["Phi"].astype(dt)
     QiPhi = Q_inv @ Phi
     PhiTQi = Phi.T @ Q_inv
-    eye = np.eye(d)
+    eye = np.eye(d, dtype=dt)
     M = np.ascontiguousarray(np.swapaxes(X_mean[:, :, 2:], 0, 1))      # (T, n, 2r) current
     st = _slice_stats(M, r)
     for i in (range(n) if nodes is None else nodes):
@@ -267,11 +269,11 @@ def sweep_stats(Y, X_mean, X_cov, params, variant, lr, nodes=None):
               st[3] - np.einsum("ta,tb->tab", Uo, Uo), st[4] - np.einsum("ta,tb->tab", Vo, Vo),
               st[5] - np.einsum("ta,tb->tab", Vo, Uo)]
         P = _p_obs(ex, R_inv, r)
-        yi = np.asarray(Y[i], dtype=np.float64).transpose(1, 2, 0)     # (T, 2, n)
+        yi = np.asarray(Y[i], dtype=dt).transpose(1, 2, 0)             # (T, 2, n)
         z = np.matmul(R_inv, yi)                                        # z_ij = R^-1 y_ij
         z[:, :, i] = 0.0                                                # j != i
         zM = np.matmul(z, M)                                            # (T, 2, 2r)
-        h = np.empty((T, d))
+        h = np.empty((T, d), dtype=dt)
         h[:, :2] = z.sum(2)
         h[:, 2:2 + r] = zM[:, 0, r:]                                    # sum z0 V_j
         h[:, 2 + r:] = zM[:, 1, :r]                                     # sum z1 U_j
@@ -284,19 +286,20 @@ def sweep_stats(Y, X_mean, X_cov, params, variant, lr, nodes=None):
         if variant == "naive":
             C = np.zeros_like(P)
             idx = np.arange(d)
-            C[:, idx, idx] = 1.0 / (P[:, idx, idx] + 1e-8)
+            C[:, idx, idx] = dt.type(1.0) / (P[:, idx, idx] + dt.type(1e-8))
             G = Pinv
         else:
             C = Pinv.copy()
             if variant == "bad":
                 C[:, :2, 2:] = 0.0
                 C[:, 2:, :2] = 0.0
-            C = (C + np.swapaxes(C, 1, 2)) / 2.0 + eye * 1e-6
+            C = (C + np.swapaxes(C, 1, 2)) / dt.type(2) + eye * dt.type(1e-6)
             G = C
+        lr_, om_ = dt.type(lr), dt.type(1.0 - lr)
         for t in range(T):
-            ht = h[t] + (QiPhi @ X_mean[i, t - 1] if t > 0 else 0.0)
-            X_mean[i, t] = lr * (G[t] @ ht) + (1.0 - lr) * X_mean[i, t]
-        X_cov[i] = lr * C + (1.0 - lr) * X_cov[i]
+            ht = h[t] + (QiPhi @ X_mean[i, t - 1] if t > 0 else dt.type(0))
+            X_mean[i, t] = lr_ * (G[t] @ ht) + om_ * X_mean[i, t]
+        X_cov[i] = lr_ * C + om_ * X_cov[i]
         new = X_mean[i, :, 2:]
         Un, Vn = new[:, :r], new[:, r:]
         st = [st[0], ex[1] + Un, ex[2] + Vn, ex[3] + np.einsum("ta,tb->tab", Un, Un),
@@ -402,15 +405,18 @@ def recon_error(Y, X_mean):
     return tot / (n * (n - 1) * T)
 
 
-def elbo_recon_fast(Y, X_mean, X_cov, params, variant):
+def elbo_recon_fast(Y, X_mean, X_cov, params, variant, dtype=np.float64):
     """elbo_split + recon_error of the same state, vectorised per slice in fp64
     (whole n x n residual matrices instead of index gathers; the entropy's
     log-determinants batched).  Same formulas as above (structured_mf.py:124-209,
     naive_mf.py:114-191, temporal_ame.py:255-291); pinned to them in
-    tests/test_oracle_fast.py.  Returns (split[4], recon)."""
+    tests/test_oracle_fast.py.  Returns (split[4], recon).  `dtype` is the
+    elementwise arithmetic type (fp64: the parity oracle; fp32: bench.py's CPU
+    baseline in the reference's dtype); the sums are Python floats either way."""
+    dt = np.dtype(dtype)
     n, T, d = X_mean.shape
     r = (d - 2) // 2
-    R_inv = params["R_inv"].astype(np.float64)
+    R_inv = params["R_inv"].astype(dt)
     p, q, q2, s = R_inv[0, 0], R_inv[0, 1], R_inv[1, 0], R_inv[1, 1]
     logdetR = _logdet(params["R"])
     trRi = float(np.trace(R_inv))
@@ -421,8 +427,8 @@ def elbo_recon_fast(Y, X_mean, X_cov, params, variant):
     CH = 8                                    # slices per gather: whole cache lines of Y
     for t in range(T):
         if t % CH == 0:
-            yc = np.ascontiguousarray(np.moveaxis(Y[:, :, t:t + CH, :], 2, 0), dtype=np.float64)
-        x = X_mean[:, t].astype(np.float64)
+            yc = np.ascontiguousarray(np.moveaxis(Y[:, :, t:t + CH, :], 2, 0), dtype=dt)
+        x = X_mean[:, t].astype(dt)
         add = x[:, 0][:, None] + x[:, 1][None, :]
         mult = x[:, 2:2 + r] @ x[:, 2 + r:].T
         m0 = add + mult                       # mean of y_ij[0]
@@ -436,10 +442,10 @@ def elbo_recon_fast(Y, X_mean, X_cov, params, variant):
     if variant == "naive":
         corr = 0.0
     else:
-        tr = np.trace(X_cov.astype(np.float64), axis1=2, axis2=3)      # (n, T)
+        tr = np.trace(X_cov.astype(dt), axis1=2, axis2=3)              # (n, T)
         corr = 0.1 * trRi / d * (n - 1) * float(tr.sum())
     loglik = -0.5 * (npairs * (logdetR + 2 * LOG2PI) + quad_sum + corr)
-    sign, ld = np.linalg.slogdet(X_cov.astype(np.float64).reshape(-1, d, d))
+    sign, ld = np.linalg.slogdet(X_cov.astype(dt).reshape(-1, d, d))
     ld = np.where(sign > 0, ld, np.where(sign == 0, -np.inf, np.nan))
     ent = float(np.sum(0.5 * (d * (1 + LOG2PI) + ld)))
     split = np.array([loglik, log_prior_initial(X_mean, X_cov, params),

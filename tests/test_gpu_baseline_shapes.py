@@ -12,7 +12,9 @@
   against the direct fp64 / fp32 restatement; the device ELBO / MSE of the
   full state against the oracle's ELBO of the same state;
 * config 4's per-rank shape (n=1024, T_local=64, r=16): two time-sharded
-  ranks on one GPU reproduce the single-process T=128 run bit for bit.
+  ranks on one GPU reproduce the single-process T=128 run bit for bit;
+* config 4 at full T (n=1024, T=512, r=16) in one process: the third sweep,
+  all 1024 x 512, against the fp64 oracle's replay.
 
 Reference: structured_mf.py:211-326 (sweep), :115-209 (ELBO),
 naive_mf.py:207-282, temporal_ame.py:255-291 (MSE).
@@ -333,14 +335,18 @@ def test_config5_rank_shape(method, gpu_device):
     assert abs(h["reconstruction_error"][-1] - e["recon"]) <= 5e-6 * e["recon"]
 
 
-# ---------------- config 4 at full T on one GPU: oracle prefix ----------------
+# ---------------- config 4 at full T on one GPU: full oracle replay ----------------
 @pytest.mark.timeout(600)
-def test_config4_full_T_oracle_prefix(gpu_device):
+def test_config4_full_T_oracle(gpu_device):
     """BASELINE config 4 (n=1024, T=512, r=16, lr=0.01) in one process: the
-    512 slices run as consecutive slice groups.  The third sweep's first K=8
-    nodes of ALL 512 slices against the fp64 oracle's replay, and the device
-    ELBO / MSE against the CPU ELBO of the device state.
+    512 slices run as consecutive slice groups.  The third sweep -- ALL 1024
+    nodes x 512 slices, means and covariances -- against the fp64 oracle's
+    replay of that sweep from the device's state after two iterations
+    (ame_oracle.sweep_stats, pinned in tests/test_oracle_fast.py), with config
+    3's bounds; the first K=8 nodes also against the direct fp64 / fp32
+    restatement; the device ELBO / MSE against the CPU ELBO of the device state.
     Reference: structured_mf.py:211-326, :115-209, temporal_ame.py:255-291."""
+    import ame_oracle as O
     from elbo_check import elbo_and_mse
     from ame_amd import TemporalAMEModel
     n, T, r, lr, K = 1024, 512, 16, 0.01, 8
@@ -355,6 +361,18 @@ def test_config4_full_T_oracle_prefix(gpu_device):
     Y32 = m.Y.cpu().numpy()
     rm, rc, rm32 = _replay_prefix(Y32, x2, c2, _params(m), _params(m, np.float32), "good", lr, K, T)
     _check_prefix(got_m[:K], got_c[:K], rm, rc, rm32)
+    Xm, Xc = x2.astype(np.float64), c2.astype(np.float64)
+    del x2, c2
+    for a in range(0, n, 256):   # chunks, with a progress line
+        O.sweep_stats(Y32, Xm, Xc, _params(m), "good", lr, nodes=range(a, min(n, a + 256)))
+        print(f"config 4: oracle replay at node {min(n, a + 256)} of {n}", flush=True)
+    err_all = np.abs(got_m.astype(np.float64) - Xm).max()
+    cerr_all = np.abs(got_c.astype(np.float64) - Xc).max()
+    print(f"config 4 full sweep (1024 x 512) vs fp64 oracle: max|dmean| {err_all:.3e} "
+          f"(max|mean| {np.abs(Xm).max():.3f}), max|dcov| {cerr_all:.3e}")
+    assert err_all <= 5e-6 * max(1.0, np.abs(Xm).max()), err_all
+    assert cerr_all <= 1e-6 * max(1.0, np.abs(Xc).max()), cerr_all
+    del Xm, Xc
     e = elbo_and_mse(Y32, got_m, got_c, _params(m), "good")
     assert abs(float(h["elbo"][-1]) - e["elbo"]) <= 5e-6 * abs(e["elbo"]), (float(h["elbo"][-1]), e)
     assert abs(h["reconstruction_error"][-1] - e["recon"]) <= 5e-6 * e["recon"]

@@ -48,12 +48,17 @@ def _check_vs_oracle(n, T, r, method, lr, dev, iters=2, **opts):
     fp32_err = np.abs(Xm32.astype(np.float64) - Xm).max()
     h = vi.fit(max_iter=iters, tolerance=0.0, verbose=False)
     err = np.abs(vi.X_mean.numpy() - Xm).max()
-    # fp32 allowance: twice the fp32 restatement's own deviation from fp64.  Two
-    # fp32 evaluations that differ only in rounding order land on either side of
-    # each other: on (64, 3, 8, good, 0.5) the kernel's error is 0.56x the fp32
-    # oracle's with the damping FMA-contracted and 1.11x with it rounded as the
-    # reference does (tools/parity_margin.py)
-    assert err <= max(5e-6 * max(1.0, np.abs(Xm).max()), 2.0 * fp32_err), (err, fp32_err)
+    # fp32 allowance: the kernel's error may exceed the fp32 restatement's own
+    # deviation from fp64 by the measured rounding-order spread plus a margin.
+    # Two fp32 evaluations that differ only in rounding order land on either
+    # side of each other: measured ratios err / fp32_err were 0.56 (damping
+    # FMA-contracted), 1.11 (rounded as the reference does) on (64, 3, 8, good,
+    # 0.5) and 1.31 on kind 20 (tools/parity_margin.py); the bound
+    # is 1.5x, and every case prints its ratio
+    ratio = err / fp32_err if fp32_err > 0 else 0.0
+    print(f"parity {n}x{T} r={r} {method}: err {err:.3e}, fp32 restatement {fp32_err:.3e}, "
+          f"ratio {ratio:.2f}")
+    assert err <= max(5e-6 * max(1.0, np.abs(Xm).max()), 1.5 * fp32_err), (err, fp32_err, ratio)
     cerr = np.abs(vi.X_cov.numpy() - Xc).max()
     assert cerr <= 1e-6 * max(1.0, np.abs(Xc).max()), cerr
     for a, b in zip(h["elbo"], ref["elbo"]):
