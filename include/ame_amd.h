@@ -70,6 +70,11 @@ enum ame_variant { AME_GOOD = 0, AME_BAD = 1, AME_NAIVE = 2 };
  *   AME_SWEEP_V2_HBM      same, (U,V) block in HBM (args.work)
  *   AME_SWEEP_V2_WORKERS  v2 plus seven GEMV worker workgroups per slice holding
  *                         the (U,V) block in registers (partial ring in args.work)
+ *   AME_SWEEP_V2_PIPE     v2 plus four GEMV worker workgroups per slice (5 per
+ *                         slice): two launches of up to half the co-resident
+ *                         slices fit at once and the kernel orders itself slice
+ *                         by slice (done flags, wait_epoch), so sweeps and slice
+ *                         groups pipeline like AME_SWEEP_V3; d > 64, n <= 4096
  * Requests (resolved by ame_sweep_kind for given dims):
  *   AME_SWEEP_AUTO        V3 when the shape fits it, else AME_SWEEP_V2_AUTO
  *   AME_SWEEP_V2_AUTO     V2_WORKERS when their workgroups are co-resident, else
@@ -83,8 +88,14 @@ enum ame_sweep_kind_code {
     AME_SWEEP_V3 = 3,
     AME_SWEEP_V2_LDS = 20,
     AME_SWEEP_V2_HBM = 21,
-    AME_SWEEP_V2_WORKERS = 22
+    AME_SWEEP_V2_WORKERS = 22,
+    AME_SWEEP_V2_PIPE = 23
 };
+
+/* ame_sweep_args.flags */
+#define AME_SWEEP_FLAG_NEXT_GROUP 1u   /* done[T_local] is the next slice group's first slice
+                                          (same rank): with wait_epoch, the last slice also
+                                          waits for it, as for any other right neighbour */
 
 /* ELBO pair kernels (ame_elbo_args.pairs_kernel): AUTO = V2 (LDS-DMA rows). */
 enum ame_pairs_kernel_code { AME_PAIRS_AUTO = 0, AME_PAIRS_V1 = 1, AME_PAIRS_V2 = 2 };
@@ -119,7 +130,7 @@ typedef struct ame_sweep_args {
     double* work;                /* scratch, >= ame_sweep_work_size() doubles: 0 for the v3
                                     sweep; the GEMV workers' partial ring (zeroed by the call
                                     itself) and the right-neighbour AR terms (filled by the call)
-                                    for v2 with workers (kind 22: n = 4096, r = 32, ...);
+                                    for v2 with workers (kinds 22 / 23: n = 4096, r = 32, ...);
                                     [T_local][n][2r] fp32 (U,V) copy when v2 keeps the slice in
                                     HBM without workers (kind 21); may be NULL
                                     when the size is 0 */
@@ -140,7 +151,7 @@ typedef struct ame_sweep_args {
     int32_t kind;                /* enum ame_sweep_kind_code: the kernel the caller sized the
                                     buffers for (normally the concrete kind ame_sweep_kind
                                     returned); a request it does not resolve to is rejected */
-    uint32_t pad_;               /* zero */
+    uint32_t flags;              /* AME_SWEEP_FLAG_* (0 for one launch over all local slices) */
     uint64_t work_doubles;       /* size of `work` in doubles, checked against
                                     ame_sweep_work_size(dims, kind) */
 } ame_sweep_args;

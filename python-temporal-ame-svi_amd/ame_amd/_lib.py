@@ -20,7 +20,8 @@ AME_STATUS_STALE_EPOCH = 8
 AME_PEER_HANDLE_BYTES = 64
 # sweep kernel requests / kinds (enum ame_sweep_kind_code)
 AME_SWEEP_AUTO, AME_SWEEP_V2_SINGLE, AME_SWEEP_V2_AUTO, AME_SWEEP_V3 = 0, 1, 2, 3
-AME_SWEEP_V2_LDS, AME_SWEEP_V2_HBM, AME_SWEEP_V2_WORKERS = 20, 21, 22
+AME_SWEEP_V2_LDS, AME_SWEEP_V2_HBM, AME_SWEEP_V2_WORKERS, AME_SWEEP_V2_PIPE = 20, 21, 22, 23
+AME_SWEEP_FLAG_NEXT_GROUP = 1
 # ELBO pair kernels (enum ame_pairs_kernel_code)
 AME_PAIRS_AUTO, AME_PAIRS_V1, AME_PAIRS_V2 = 0, 1, 2
 
@@ -40,7 +41,7 @@ class ame_sweep_args(ctypes.Structure):
                 ("one_minus_lr", ctypes.c_float), ("epoch", ctypes.c_uint32), ("status", c_vp),
                 ("work", c_vp), ("cov_new", c_vp), ("done", c_vp),
                 ("wait_epoch", ctypes.c_uint32), ("back_out", c_vp), ("back_in", c_vp),
-                ("kind", c_int32), ("pad_", ctypes.c_uint32), ("work_doubles", ctypes.c_uint64)]
+                ("kind", c_int32), ("flags", ctypes.c_uint32), ("work_doubles", ctypes.c_uint64)]
 
 
 class ame_cov_args(ctypes.Structure):

@@ -8,7 +8,7 @@
 
 int ame_sweep_dispatch(const ame_dims*, const ame_sweep_args*, hipStream_t);
 int ame_sweep_blocks_per_cu(int n, int r, int mode);
-int ame_sweep_workers_fit(const ame_dims* dm);
+int ame_sweep_workers_fit(const ame_dims* dm, int mode);   // mode 2: kind 22, 3: kind 23
 int ame_sweep3_dispatch(const ame_dims*, const ame_sweep_args*, hipStream_t);
 int ame_sweep3_supported(int n, int r);
 int ame_sweep3_blocks_per_cu(int n, int r);
@@ -192,7 +192,8 @@ static int device_cus() {
 static bool v2_block_in_lds(int n, int r) { return !sweep_lds_layout(n, r, 0).m_global; }
 static bool v2_single_fits(int n, int r) { return sweep_lds_layout(n, r, 1).total <= AME_LDS_MAX; }
 static bool is_concrete(int k) {
-    return k == AME_SWEEP_V3 || k == AME_SWEEP_V2_LDS || k == AME_SWEEP_V2_HBM || k == AME_SWEEP_V2_WORKERS;
+    return k == AME_SWEEP_V3 || k == AME_SWEEP_V2_LDS || k == AME_SWEEP_V2_HBM || k == AME_SWEEP_V2_WORKERS ||
+           k == AME_SWEEP_V2_PIPE;
 }
 
 // Request -> concrete kernel for these dims (-1 + message when it cannot run).
@@ -205,7 +206,7 @@ static int resolve_kind(const ame_dims* d, int request) {
             if (ame_sweep3_supported(n, r)) return AME_SWEEP_V3;
             // fall through
         case AME_SWEEP_V2_AUTO:
-            if (ame_sweep_workers_fit(d)) return AME_SWEEP_V2_WORKERS;
+            if (ame_sweep_workers_fit(d, 2)) return AME_SWEEP_V2_WORKERS;
             // fall through
         case AME_SWEEP_V2_SINGLE:
             if (v2_block_in_lds(n, r)) return AME_SWEEP_V2_LDS;
@@ -221,8 +222,12 @@ static int resolve_kind(const ame_dims* d, int request) {
             if (v2_single_fits(n, r)) return AME_SWEEP_V2_HBM;
             return fail("ame_sweep: the v2 sweep does not fit n=%d, r=%d", n, r);
         case AME_SWEEP_V2_WORKERS:
-            if (ame_sweep_workers_fit(d)) return AME_SWEEP_V2_WORKERS;
+            if (ame_sweep_workers_fit(d, 2)) return AME_SWEEP_V2_WORKERS;
             return fail("ame_sweep: GEMV workers do not fit n=%d, T_local=%d", n, d->T_local);
+        case AME_SWEEP_V2_PIPE:
+            if (ame_sweep_workers_fit(d, 3)) return AME_SWEEP_V2_PIPE;
+            return fail("ame_sweep: the pipelined GEMV-worker sweep does not fit n=%d, T_local=%d",
+                        n, d->T_local);
         default:
             return fail("ame_sweep: unknown sweep kind request %d", request);
     }
@@ -235,6 +240,7 @@ long long ame_sweep_lds_bytes(int n, int r, int kind) {
         case AME_SWEEP_V2_LDS: return ame_v2_mode_lds(n, r, 0);
         case AME_SWEEP_V2_HBM: return ame_v2_mode_lds(n, r, 1);
         case AME_SWEEP_V2_WORKERS: return ame_v2_mode_lds(n, r, 2);
+        case AME_SWEEP_V2_PIPE: return ame_v2_mode_lds(n, r, 3);
         default: return 0;
     }
 }
@@ -258,13 +264,24 @@ int ame_sweep_max_slices(int n, int r, int request) {
             return v2_single_fits(n, r) ? ame_sweep_blocks_per_cu(n, r, 1) * cus : 0;
         case AME_SWEEP_V2_WORKERS:
             return ame_sweep_blocks_per_cu(n, r, 2) * cus / (1 + AME_GW);
+        case AME_SWEEP_V2_PIPE: {
+            ame_dims one = {n, r, 1, 0, 1, 0};
+            if (!ame_sweep_workers_fit(&one, 3)) return 0;
+            return ame_sweep_blocks_per_cu(n, r, 3) * cus / (1 + AME_GW_P);
+        }
         default:
             return 0;
     }
 }
 
 int ame_sweep_orders_slices(int n, int r, int kind) {
-    return r_supported(r) && kind == AME_SWEEP_V3 && ame_sweep3_supported(n, r) ? 1 : 0;
+    if (!r_supported(r) || n < 2) return 0;
+    if (kind == AME_SWEEP_V3) return ame_sweep3_supported(n, r) ? 1 : 0;
+    if (kind == AME_SWEEP_V2_PIPE) {
+        ame_dims one = {n, r, 1, 0, 1, 0};
+        return ame_sweep_workers_fit(&one, 3) ? 1 : 0;
+    }
+    return 0;
 }
 
 int ame_sweep_kind(const ame_dims* dims, int request) {
@@ -280,7 +297,8 @@ long long ame_sweep_work_size(const ame_dims* dims, int kind) {
         // [T_local][n][2r] fp32 (U,V) copy
         case AME_SWEEP_V2_HBM: return ((long long)dims->T_local * dims->n * 2 * dims->r + 1) / 2;
         // partial ring, then the precomputed right AR terms
-        case AME_SWEEP_V2_WORKERS: return ame_v2_ring_doubles(dims) + ame_v2_arr_doubles(dims);
+        case AME_SWEEP_V2_WORKERS: return ame_v2_ring_doubles(dims, 2) + ame_v2_arr_doubles(dims);
+        case AME_SWEEP_V2_PIPE: return ame_v2_ring_doubles(dims, 3) + ame_v2_arr_doubles(dims);
         default: return fail("ame_sweep_work_size: %d is not a concrete sweep kind", kind);
     }
 }
@@ -315,8 +333,9 @@ int ame_sweep(const ame_dims* dims, const ame_sweep_args* a, void* stream) {
         return fail("ame_sweep: the work buffer holds %d doubles, kind %d needs more", (int)a->work_doubles, kind);
     if (a->wait_epoch != 0 && (!ame_sweep_orders_slices(dims->n, dims->r, kind) || !a->done))
         return fail("ame_sweep: wait_epoch needs a kernel that orders slices (kind %d) and a done array", kind);
-    const int maxs = kind == AME_SWEEP_V2_WORKERS ? dims->T_local
-                                                   : ame_sweep_max_slices(dims->n, dims->r, kind);
+    const int maxs = (kind == AME_SWEEP_V2_WORKERS || kind == AME_SWEEP_V2_PIPE)
+                          ? dims->T_local   // resolve_kind checked that the launch co-resides
+                          : ame_sweep_max_slices(dims->n, dims->r, kind);
     if (dims->T_local > maxs)
         return fail("ame_sweep: T_local=%d exceeds co-resident workgroups (%d)", dims->T_local, maxs);
     ame_sweep_args c = *a;

@@ -128,6 +128,16 @@ __host__ __device__ inline SweepLds sweep_lds_layout(int n, int R, int force_glo
 #define AME_GW 7          // GEMV worker workgroups per slice
 #define AME_GW_RING 8     // partial ring slots per worker
 #define AME_GW_MAXPW 152  // nodes per worker wave held in registers: n <= 7 * 4 * 152
+// pipelined v2 sweep (kind AME_SWEEP_V2_PIPE, MODE 3): four workers per slice,
+// so a slice is 5 workgroups and two consecutive launches of up to 25 slices
+// (one workgroup per CU) are co-resident.  Three workers (344 nodes per worker
+// wave at n = 4096) spill ~1 000 VGPRs at every split between registers and
+// LDS tried; four (256 per wave) compile spill-free
+#define AME_GW_P 4
+#define AME_GW_P_MAXPW 256   // n <= 4 * 4 * 256
+#define AME_GW_P_NREG 256    // of which in registers; the rest (none) in the worker's LDS
+__host__ __device__ inline int ame_v2_nworkers(int mode) { return mode == 3 ? AME_GW_P : AME_GW; }
+__host__ __device__ inline int ame_v2_maxpw(int mode) { return mode == 3 ? AME_GW_P_MAXPW : AME_GW_MAXPW; }
 
 // Tag of worker partial m of sweep `epoch` in the partial ring.  Bit 31 is
 // always set, so a slot the launch zeroed can never match (an all-zero word
@@ -137,23 +147,24 @@ __host__ __device__ inline uint32_t ame_gw_tag(uint32_t epoch, int m) {
     return 0x80000000u | ((epoch & 0x7FFFu) << 16) | ((uint32_t)m & 0xFFFFu);
 }
 
-// LDS of one v2 slice workgroup per mode (0: (U,V) in LDS, 1: in HBM, 2: workers)
-// and of a GEMV worker workgroup; a MODE 2 launch sizes for the larger
-__host__ __device__ inline long long ame_v2_worker_lds(int n, int R) {
-    const int NW = (n + AME_GW - 1) / AME_GW, ZN = 4 * AME_GW_MAXPW;
-    return ame_align16(8LL * (NW > ZN ? NW : ZN)) + 4LL * 4 * (2 * R + 2);
+// LDS of one v2 slice workgroup per mode (0: (U,V) in LDS, 1: in HBM, 2 / 3:
+// workers) and of a GEMV worker workgroup; a worker launch sizes for the larger
+__host__ __device__ inline long long ame_v2_worker_lds(int n, int R, int mode = 2) {
+    const int nw = ame_v2_nworkers(mode);
+    const int NW = (n + nw - 1) / nw, ZN = 4 * ame_v2_maxpw(mode);
+    // zb, red, and (MODE 3) the LDS-held node slots [4 waves][MAXPW - NREG][64]
+    const long long mld = mode == 3 ? 4LL * 4 * (AME_GW_P_MAXPW - AME_GW_P_NREG) * 64 : 0;
+    return ame_align16(8LL * (NW > ZN ? NW : ZN)) + ame_align16(4LL * 4 * (2 * R + 2)) + mld;
 }
 __host__ __device__ inline long long ame_v2_mode_lds(int n, int R, int mode) {
-    const long long m = sweep_lds_layout(n, R, mode != 0 ? 1 : 0, mode == 2 ? 1 : 0).total;
-    if (mode != 2) return m;
-    const long long w = ame_v2_worker_lds(n, R);
+    const long long m = sweep_lds_layout(n, R, mode != 0 ? 1 : 0, mode >= 2 ? 1 : 0).total;
+    if (mode < 2) return m;
+    const long long w = ame_v2_worker_lds(n, R, mode);
     return m > w ? m : w;
 }
-__host__ __device__ inline long long ame_v2_ring_doubles(const ame_dims* d) {
-    return (long long)d->T_local * AME_GW * AME_GW_RING * (2 * d->r + 2);
+__host__ __device__ inline long long ame_v2_ring_doubles(const ame_dims* d, int mode = 2) {
+    return (long long)d->T_local * ame_v2_nworkers(mode) * AME_GW_RING * (2 * d->r + 2);
 }
-// MODE 2: the precomputed right-neighbour AR terms, [T_local][n][NPA * d] past the
-// ring (NPA = AR row parts on 192 threads: ArPart<R, true> in ame_sweep.hip)
 __host__ __device__ inline long long ame_v2_arr_doubles(const ame_dims* d) {
     const int D = 2 + 2 * d->r, npa = (4 * D <= 192) ? 4 : 2;
     return (long long)d->T_local * d->n * npa * D;

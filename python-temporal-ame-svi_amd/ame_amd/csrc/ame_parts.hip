@@ -6,7 +6,7 @@
 #define AME_DECL_SWEEP(P)                                                                 \
     int ame_sweep_dispatch_p##P(const ame_dims*, const ame_sweep_args*, hipStream_t);     \
     int ame_sweep_blocks_per_cu_p##P(int, int, int);                                      \
-    int ame_sweep_workers_fit_p##P(const ame_dims*);
+    int ame_sweep_workers_fit_p##P(const ame_dims*, int);
 AME_DECL_SWEEP(0)
 AME_DECL_SWEEP(1)
 AME_DECL_SWEEP(2)
@@ -33,11 +33,11 @@ int ame_sweep_blocks_per_cu(int n, int r, int mode) {
         default: return ame_sweep_blocks_per_cu_p2(n, r, mode);
     }
 }
-int ame_sweep_workers_fit(const ame_dims* dm) {
+int ame_sweep_workers_fit(const ame_dims* dm, int mode) {
     switch (dm->r % 3) {
-        case 0: return ame_sweep_workers_fit_p0(dm);
-        case 1: return ame_sweep_workers_fit_p1(dm);
-        default: return ame_sweep_workers_fit_p2(dm);
+        case 0: return ame_sweep_workers_fit_p0(dm, mode);
+        case 1: return ame_sweep_workers_fit_p1(dm, mode);
+        default: return ame_sweep_workers_fit_p2(dm, mode);
     }
 }
 int ame_sweep3_dispatch(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {

@@ -195,6 +195,59 @@ struct ArPart {
     static constexpr int MC = (D + NPA - 1) / NPA;
 };
 
+// Pipelined launch (MODE 3, wait_epoch != 0): every workgroup of slice t -- the
+// slice's own and its GEMV workers -- reads the previous sweep's outputs for
+// slices t and t+1 (old means, covariances; slice t+1 also reads the hand-off
+// granules this sweep overwrites), so it starts only once that sweep flagged
+// both done: done[t], done[t+1] (done[T_local] when the next slice group
+// follows, AME_SWEEP_FLAG_NEXT_GROUP), or for the rank's last slice the right
+// rank's back-channel done word.  Same epoch window as ame_sweep3.hip: a flag
+// above wait_epoch cannot be current and sets AME_STATUS_STALE_EPOCH.
+__device__ __forceinline__ void ame_v2_wait_prev(const ame_sweep_args& a, int t, int TL, bool back_rd,
+                                                 int nd /* n * d: the back channel's done word */) {
+    if (a.wait_epoch == 0u) return;
+    if (threadIdx.x == 0) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        const int qn = (t + 1 < TL || (a.flags & AME_SWEEP_FLAG_NEXT_GROUP)) ? 2 : 1;
+        for (int q = 0; q < qn; ++q) {
+            while (true) {
+                const uint32_t dv = __hip_atomic_load(a.done + t + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (dv > a.wait_epoch) {
+                    atomicOr(a.status, AME_STATUS_STALE_EPOCH);
+                    break;
+                }
+                if (dv == a.wait_epoch) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > AME_SPIN_TICKS_LOCAL) {
+                    atomicOr(a.status, AME_STATUS_SPIN_TIMEOUT);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(8);
+            }
+        }
+        if (back_rd) {   // the right rank's first slice of the previous sweep
+            const uint32_t* bd = (const uint32_t*)(a.back_in + AME_BACK_DONE_OFFSET(nd));
+            while (true) {
+                const uint32_t dv = __hip_atomic_load(const_cast<uint32_t*>(bd), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_SYSTEM);
+                if (dv > a.wait_epoch) {
+                    atomicOr(a.status, AME_STATUS_STALE_EPOCH);
+                    break;
+                }
+                if (dv == a.wait_epoch) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > AME_SPIN_TICKS_HALO) {
+                    atomicOr(a.status, AME_STATUS_HALO_TIMEOUT);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(8);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+}
+
 // GEMV worker (MODE 2): workgroup TL + t*AME_GW + g owns nodes
 // [g*NW, (g+1)*NW) of slice t, NW = ceil(n / AME_GW); wave q holds nodes
 // base + q + 4s (s < AME_GW_MAXPW), lane c column c of (U,V), in registers.
@@ -203,28 +256,36 @@ struct ArPart {
 //   part[2r + p] = sum z_mj[p]
 // with node j's new mean for j <= m-4 (read from the slice's hand-off
 // granules, which the slice's workgroup stores when it publishes node j).
-template <int R>
-__device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_args& a, char* smem) {
+template <int R, int MODE>
+__device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_args& a, char* smem,
+                                            const int t, const int g) {
     constexpr int D = 2 + 2 * R, M2 = 2 * R, PW = M2 + 2;
+    // MODE 2: seven workers per slice (kind 22); MODE 3: four (kind 23, pipelined)
+    constexpr int NG = (MODE == 3) ? AME_GW_P : AME_GW;
+    constexpr int MAXPW = (MODE == 3) ? AME_GW_P_MAXPW : AME_GW_MAXPW;
     const int n = dm.n, TL = dm.T_local;
-    const int w = (int)blockIdx.x - TL, t = w / AME_GW, g = w - t * AME_GW;
-    const int NW = (n + AME_GW - 1) / AME_GW, base = g * NW;
+    const int NW = (n + NG - 1) / NG, base = g * NW;
     const int cnt = max(0, min(n, base + NW) - base);
     const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6;
     const int npw = (cnt > q) ? (cnt - q + 3) / 4 : 0;
     // z of the range; entries past it stay zero, so the GEMV reads every
     // register slot's z unconditionally (loads can be batched)
-    constexpr int ZN = 4 * AME_GW_MAXPW;
+    constexpr int ZN = 4 * MAXPW;
     float2* zb = (float2*)smem;                                   // [max(NW, ZN)]
     float* red = (float*)(smem + ame_align16(8LL * (NW > ZN ? NW : ZN)));   // [4][PW]
     const float* xo = a.x_old + (size_t)t * n * D;
     const uint64_t* hand = a.hand + (size_t)t * n * D;
-    uint64_t* hp = (uint64_t*)a.work + (size_t)(t * AME_GW + g) * AME_GW_RING * PW;
+    uint64_t* hp = (uint64_t*)a.work + (size_t)(t * NG + g) * AME_GW_RING * PW;
     const int nys = ame_ystride(n);
     const float* ysl = a.Yt + (size_t)t * n * nys * 2;
     const float r00f = (float)a.rinv[0], r01f = (float)a.rinv[1], r10f = (float)a.rinv[2], r11f = (float)a.rinv[3];
     const bool col = lane < M2;
     bool dead = false;
+    // MODE 3, pipelined launch: this worker's inputs (old means of slices t and
+    // t+1) are the previous sweep's outputs -- wait for its done flags as the
+    // slice's workgroup does (ame_v2_wait_prev)
+    const bool back_rd = (MODE == 3) && (a.wait_epoch != 0u) && (t == TL - 1) && (a.back_in != nullptr);
+    if constexpr (MODE == 3) ame_v2_wait_prev(a, t, TL, back_rd, n * D);
     // Right-neighbour AR terms PhiTQi mu_{j,t+1}^old of this worker's nodes, for
     // the slice workgroup's phase 2 (same products, order and zero padding as
     // its in-sweep form): formed here, before partial 0, and released with it --
@@ -244,9 +305,12 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
             c[mm] = (m < D) ? a.consts[4 * DD + (size_t)k * D + m] : 0.0;
         }
         float* ms = (float*)zb;
-        double* outp = a.work + ame_v2_ring_doubles(&dm) + ((size_t)t * n + base) * (NPA * D);
+        double* outp = a.work + ame_v2_ring_doubles(&dm, MODE) + ((size_t)t * n + base) * (NPA * D);
+        // old means of slice t+1: the next local slice; for the last local slice
+        // next_old, or in a pipelined launch the right rank's back channel
         const float* src = (tg >= Tt - 1) ? nullptr
                          : (t < TL - 1) ? a.x_old + ((size_t)(t + 1) * n + base) * D
+                         : back_rd      ? a.back_in + (size_t)base * D
                                         : a.next_old + (size_t)base * D;
         for (int j0 = 0; j0 < cnt; j0 += NB) {
             const int nb = min(NB, cnt - j0);
@@ -269,15 +333,24 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // before any partial store
     }
-    float mreg[AME_GW_MAXPW];
+    // MODE 3 may hold more slots per wave than registers allow: the first NREG in
+    // registers, the rest
+    // in this workgroup's LDS past zb / red ([wave][slot][lane], conflict-free)
+    constexpr int NREG = (MODE == 3) ? AME_GW_P_NREG : MAXPW, NLD = MAXPW - NREG;
+    float* mld = (float*)(smem + ame_align16(8LL * (NW > ZN ? NW : ZN)) + ame_align16(4LL * 4 * PW));
+    float mreg[NREG];
 #pragma unroll
-    for (int s2 = 0; s2 < AME_GW_MAXPW; ++s2) {
+    for (int s2 = 0; s2 < NREG; ++s2) {
         const int j = base + q + 4 * s2;
         mreg[s2] = (s2 < npw && col) ? xo[(size_t)j * D + 2 + lane] : 0.f;
     }
+    for (int sl = 0; sl < NLD; ++sl) {
+        const int s2 = NREG + sl, j = base + q + 4 * s2;
+        mld[(q * NLD + sl) * 64 + lane] = (s2 < npw && col) ? xo[(size_t)j * D + 2 + lane] : 0.f;
+    }
     for (int e = cnt + tid; e < ZN; e += AME_NT) zb[e] = make_float2(0.f, 0.f);
     // Y row of the next node, prefetched into registers one node ahead
-    constexpr int YQ = (4 * AME_GW_MAXPW + AME_NT - 1) / AME_NT;
+    constexpr int YQ = (4 * MAXPW + AME_NT - 1) / AME_NT;
     float2 ypf[YQ];
     auto y_prefetch = [&](int m) {
         const float2* yrow = (const float2*)(ysl + (size_t)(m < n ? m : 0) * nys * 2) + base;
@@ -334,8 +407,9 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
             }
             const float val = __uint_as_float((uint32_t)v);
 #pragma unroll
-            for (int s2 = 0; s2 < AME_GW_MAXPW; ++s2)
+            for (int s2 = 0; s2 < NREG; ++s2)
                 if (s2 == sn && col) mreg[s2] = val;
+            if (NLD > 0 && sn >= NREG && col) mld[(q * NLD + (sn - NREG)) * 64 + lane] = val;
         }
         WSTAMP(1);
         // z row of node m over the range (nodes m-3..m left out)
@@ -358,19 +432,62 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
         WSTAMP(2);
         // U_c -> h_V (z1), V -> h_U (z0); four independent chains
         float a4[4] = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (MODE == 3) {
+            // register slots in chunks of 32 (all loads ahead of the FMAs would
+            // need hundreds of temporaries beside mreg), then the LDS slots; the
+            // same products and summation order (a4[slot & 3]) throughout
+            constexpr int CH = 32;
 #pragma unroll
-        for (int s2 = 0; s2 < AME_GW_MAXPW; ++s2) {
-            const float2 z = zb[q + 4 * s2];
-            a4[s2 & 3] = fmaf(lane < R ? z.y : z.x, mreg[s2], a4[s2 & 3]);
+            for (int c0 = 0; c0 < NREG; c0 += CH) {
+                float zc[CH];
+#pragma unroll
+                for (int b = 0; b < CH; ++b) {
+                    const int s2 = c0 + b < NREG ? c0 + b : NREG - 1;
+                    const float2 z = zb[q + 4 * s2];
+                    zc[b] = lane < R ? z.y : z.x;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int b = 0; b < CH; ++b) {
+                    const int s2 = c0 + b;
+                    if (s2 < NREG) a4[s2 & 3] = fmaf(zc[b], mreg[s2], a4[s2 & 3]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            constexpr int CL = 8;
+#pragma unroll
+            for (int c0 = 0; c0 < NLD; c0 += CL) {
+                float zc[CL], mv[CL];
+#pragma unroll
+                for (int b = 0; b < CL; ++b) {
+                    const int sl = c0 + b < NLD ? c0 + b : NLD - 1;
+                    const float2 z = zb[q + 4 * (NREG + sl)];
+                    zc[b] = lane < R ? z.y : z.x;
+                    mv[b] = mld[(q * NLD + sl) * 64 + lane];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int b = 0; b < CL; ++b) {
+                    const int s2 = NREG + c0 + b;
+                    if (c0 + b < NLD) a4[s2 & 3] = fmaf(zc[b], mv[b], a4[s2 & 3]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
+#pragma unroll
+            for (int s2 = 0; s2 < MAXPW; ++s2) {
+                const float2 z = zb[q + 4 * s2];
+                a4[s2 & 3] = fmaf(lane < R ? z.y : z.x, mreg[s2], a4[s2 & 3]);
+            }
         }
         const float acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
         // sum of z over the wave's nodes: lane l takes slots l, l+64, l+128, then a
         // fixed xor tree over the wave
         float s0 = 0.f, s1 = 0.f;
 #pragma unroll
-        for (int u = 0; u < (AME_GW_MAXPW + 63) / 64; ++u) {
+        for (int u = 0; u < (MAXPW + 63) / 64; ++u) {
             const int s2 = lane + 64 * u;
-            if (s2 < AME_GW_MAXPW) {
+            if (s2 < MAXPW) {
                 const float2 z = zb[q + 4 * s2];
                 s0 += z.x;
                 s1 += z.y;
@@ -407,10 +524,36 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
 // come from x_old in that mode.
 // MODE 0: (U,V) in LDS; MODE 1: in HBM (MG); MODE 2: GEMV workers (no slice
 // block in this workgroup at all; old rows of single nodes come from x_old).
+// Block -> (slice, role) of a worker launch: role 0 is the slice's own
+// workgroup, role 1 + g its GEMV worker g.  MODE 2: the slices' workgroups
+// first, then the workers slice by slice.  MODE 3 with T_local % 8 == 0:
+// XCD-aware (workgroup b runs on XCD b % 8): each XCD holds T_local / 8
+// consecutive slices with all their workers, so hand-off granules and worker
+// partials stay in that XCD's L2.
+template <int MODE>
+__device__ __forceinline__ void v2_block_role(int TL, int& slice, int& role) {
+    constexpr int NG = (MODE == 3) ? AME_GW_P : AME_GW;
+    const int b = blockIdx.x;
+    if (MODE == 3 && (TL & 7) == 0) {
+        const int per = TL >> 3, w = b >> 3;
+        slice = (b & 7) * per + (w % per);
+        role = w / per;
+    } else if (b < TL) {
+        slice = b;
+        role = 0;
+    } else {
+        const int w = b - TL;
+        slice = w / NG;
+        role = 1 + (w - slice * NG);
+    }
+}
+
 template <int R, int MODE>
 __global__ void __launch_bounds__(AME_NT)
 ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
-    constexpr bool MG = MODE == 1, WK = MODE == 2;
+    // MODE 2: seven GEMV workers per slice (kind 22); MODE 3: four, pipelined (kind 23)
+    constexpr bool MG = MODE == 1, WK = MODE >= 2, PIPE = MODE == 3;
+    constexpr int NGW = PIPE ? AME_GW_P : AME_GW;
     constexpr int D = 2 + 2 * R, M2 = 2 * R, KS = D + 1, US = (M2 + 15) / 16;
     constexpr int KH = (D + 63) / 64;   // state rows per solver lane
     constexpr int VEC = (R % 4 == 0) ? 4 : ((R % 2 == 0) ? 2 : 1);
@@ -423,13 +566,15 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     constexpr int NLT = D * (D + 1) / 2, LTQ = (NLT + AME_NT - 1) / AME_NT;
     const int n = dm.n, TL = dm.T_local, Tt = dm.T_total;
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    int slice = blockIdx.x, role = 0;
     if constexpr (WK) {
-        if ((int)blockIdx.x >= TL) {
-            gemv_worker<R>(dm, a, smem);
+        v2_block_role<MODE>(TL, slice, role);
+        if (role > 0) {
+            gemv_worker<R, MODE>(dm, a, smem, slice, role - 1);
             return;
         }
     }
-    const int tl = blockIdx.x, tg = dm.t_begin + tl;
+    const int tl = slice, tg = dm.t_begin + tl;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const bool is_naive = dm.variant == AME_NAIVE, is_bad = dm.variant == AME_BAD;
 
@@ -498,6 +643,10 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         if constexpr (MG || WK) return xo + (size_t)j * D + 2;
         else return M + j * M2;
     };
+
+    // pipelined launch (MODE 3): the previous sweep's slices t, t+1 first
+    if constexpr (PIPE)
+        ame_v2_wait_prev(a, tl, TL, (a.wait_epoch != 0u) && (tl == TL - 1) && (a.back_in != nullptr), n * D);
 
     // ------------------------------------------------------------------
     // init: slice state, P_0 = P_const + sum_{j != 0} F_j, K_0 = P_0^-1
@@ -688,7 +837,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         const int rt = WK ? (tid >= 192 ? tid - 192 : ((tid >= 64 && tid < 64 + PW - 64) ? tid : -1)) : tid;
         if (rt >= 0 && rt < PW) {
             float acc = 0.f;
-            for (int g = 0; g < (WK ? AME_GW + 1 : GW); ++g) acc += part[g * PW + rt];
+            for (int g = 0; g < (WK ? NGW + 1 : GW); ++g) acc += part[g * PW + rt];
             gob(node)[(rt < M2) ? 2 + rt : rt - M2] = (double)acc;
         }
     };
@@ -703,7 +852,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     // node m-4 is known, so the partials of node i+1 are normally in L2 by then
     // and phase 2 mostly checks tags.  Every gather(node) must follow a
     // gather_issue(node): the entries past the partials are pre-tagged there.
-    constexpr int GNE = AME_GW * PW, GGE = (GNE + 127) / 128;
+    constexpr int GNE = NGW * PW, GGE = (GNE + 127) / 128;
     uint64_t gv[GGE];
     // raw y_{node,node-3}, y_{node,node-2} (threads ht < PW) and y_{node,node-1}
     // (ht == 0), loaded with the partials: in phase 2 they were HBM round trips
@@ -730,7 +879,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
 #pragma unroll
             for (int q = 0; q < 3; ++q) gy[q] = yr[max(node - 3 + q, 0)];
         }
-        const uint64_t* hs = (const uint64_t*)a.work + ((size_t)tl * AME_GW * AME_GW_RING + (node % AME_GW_RING)) * PW;
+        const uint64_t* hs = (const uint64_t*)a.work + ((size_t)tl * NGW * AME_GW_RING + (node % AME_GW_RING)) * PW;
 #pragma unroll
         for (int u = 0; u < GGE; ++u) gv[u] = gran_load_agent(hs + goff[u]);
     };
@@ -738,7 +887,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         const int ht = tid - 128;
         if (ht < 0) return;
         const uint32_t want = ame_gw_tag(a.epoch, node);
-        const uint64_t* hp = (const uint64_t*)a.work + (size_t)tl * AME_GW * AME_GW_RING * PW;
+        const uint64_t* hp = (const uint64_t*)a.work + (size_t)tl * NGW * AME_GW_RING * PW;
         constexpr int NE = GNE, GE = GGE;
         const uint64_t* hs = hp + (size_t)(node % AME_GW_RING) * PW;
         uint64_t (&v)[GE] = gv;   // issued by gather_issue(node)
@@ -789,7 +938,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 else if (ht < M2) acc = fmaf(z1, mj[2 + ht - R], acc);    // h_V += z1 U
                 else acc += (ht == M2) ? z0 : z1;
             }
-            part[AME_GW * PW + ht] = acc;
+            part[NGW * PW + ht] = acc;
         }
         if (ht == 0 && node >= 1) {   // j = node - 1 >= 0
             scal[40] = (double)gy[2].x;
@@ -799,7 +948,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     // WK: the PhiTQi mu_right half of node `node`, precomputed before the sweep
     // (by the GEMV workers; the work buffer past the partial ring); the QiPhi
     // mu_left half once wave 1 has polled mu_left
-    const double* arr = WK ? a.work + ame_v2_ring_doubles(&dm) + (size_t)tl * n * (NPA * D) : nullptr;
+    const double* arr = WK ? a.work + ame_v2_ring_doubles(&dm, MODE) + (size_t)tl * n * (NPA * D) : nullptr;
     auto ar_right_load = [&](int node) -> double {
         return (at >= 0 && at < NPA * D && node < n) ? arr[(size_t)node * (NPA * D) + at] : 0.0;
     };
@@ -926,7 +1075,9 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     auto right_regs = [&](int node, float& nx, float& ol) {   // threads 128..128+D
         const int k = tid - 128;
         nx = 0.f;
-        if (tg < Tt - 1)
+        // WK: the right AR terms come precomputed from the workers (mu_right is
+        // not read; next_old may be absent in a pipelined launch)
+        if (tg < Tt - 1 && !WK)
             nx = (tl < TL - 1) ? a.x_old[((size_t)(tl + 1) * n + node) * D + k]
                                : a.next_old[(size_t)node * D + k];
         ol = xo[(size_t)node * D + k];
@@ -1594,6 +1745,34 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         STAMP(3);
     }
     cov_flush(n - 1);
+    // ---- slice done: release its means, covariances and granules, then flag it
+    // for the next sweep (ame_sweep3.hip's epilogue; every wave drains its own
+    // stores first) ----
+    if (a.done != nullptr || (tl == 0 && a.back_out != nullptr)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    if (a.done != nullptr && tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(a.done + tl, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // ---- first slice of a rank with a left neighbour: its new means are that
+    // rank's next_old in the next (pipelined) sweep; system-scope release ----
+    if (tl == 0 && a.back_out != nullptr) {
+        for (int e = tid; e < n * D; e += AME_NT)
+            a.back_out[e] = __uint_as_float(__hip_atomic_load(
+                const_cast<uint32_t*>((const uint32_t*)(xn + e)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store((uint32_t*)(a.back_out + AME_BACK_DONE_OFFSET(n * D)), a.epoch,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
 }
 
 template <int R, int MODE>
@@ -1604,10 +1783,10 @@ static int launch_sweep_t(const ame_dims* dm, const ame_sweep_args* a, hipStream
         hipSuccess)
         return -2;
     int blocks = dm->T_local;
-    if constexpr (MODE == 2) {
-        blocks = dm->T_local * (1 + AME_GW);
+    if constexpr (MODE >= 2) {
+        blocks = dm->T_local * (1 + ame_v2_nworkers(MODE));
         // partial ring: zero never matches a tag (ame_gw_tag sets bit 31)
-        const size_t bytes = (size_t)ame_v2_ring_doubles(dm) * 8;
+        const size_t bytes = (size_t)ame_v2_ring_doubles(dm, MODE) * 8;
         if (hipMemsetAsync(a->work, 0, bytes, st) != hipSuccess) return -3;
         static_assert(ArPart<R, true>::NPA == ((4 * (2 + 2 * R) <= 192) ? 4 : 2),
                       "ame_v2_arr_doubles sizes the AR parts");
@@ -1630,17 +1809,18 @@ static int sweep_occupancy_t(int n) {
     return per_cu;
 }
 
-// MODE 2 can run when its T_local * (1 + AME_GW) workgroups are co-resident and
-// a worker wave's node share fits its registers
-template <int R>
+// MODE 2 / 3 can run when its T_local * (1 + workers) workgroups are co-resident
+// and a worker wave's node share fits its registers
+template <int R, int MODE>
 static bool workers_fit(int n, int T_local) {
-    const int NW = (n + AME_GW - 1) / AME_GW;
-    if ((NW + 3) / 4 > AME_GW_MAXPW || n > 65535) return false;
-    if (ame_v2_mode_lds(n, R, 2) > AME_LDS_MAX) return false;
+    const int nw = ame_v2_nworkers(MODE);
+    const int NW = (n + nw - 1) / nw;
+    if ((NW + 3) / 4 > ame_v2_maxpw(MODE) || n > 65535) return false;
+    if (ame_v2_mode_lds(n, R, MODE) > AME_LDS_MAX) return false;
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess) return false;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
-    return (long long)T_local * (1 + AME_GW) <= (long long)sweep_occupancy_t<R, 2>(n) * cus;
+    return (long long)T_local * (1 + nw) <= (long long)sweep_occupancy_t<R, MODE>(n) * cus;
 }
 
 // a->kind is concrete here (ame_capi.hip resolved and checked it)
@@ -1648,6 +1828,7 @@ template <int R>
 static int launch_sweep(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {
     switch (a->kind) {
         case AME_SWEEP_V2_WORKERS: return launch_sweep_t<R, 2>(dm, a, st);
+        case AME_SWEEP_V2_PIPE: return launch_sweep_t<R, 3>(dm, a, st);
         case AME_SWEEP_V2_HBM: return launch_sweep_t<R, 1>(dm, a, st);
         case AME_SWEEP_V2_LDS: return launch_sweep_t<R, 0>(dm, a, st);
         default: return -1;
@@ -1660,6 +1841,7 @@ static int sweep_occupancy(int n, int mode) {
         case 0: return sweep_occupancy_t<R, 0>(n);
         case 1: return sweep_occupancy_t<R, 1>(n);
         case 2: return sweep_occupancy_t<R, 2>(n);
+        case 3: return sweep_occupancy_t<R, 3>(n);
         default: return 0;
     }
 }
@@ -1686,10 +1868,11 @@ int AME_PFN(ame_sweep_blocks_per_cu)(int n, int r, int mode) {
 }
 
 // 1 when the v2 sweep with GEMV workers can run these dims
-int AME_PFN(ame_sweep_workers_fit)(const ame_dims* dm) {
+int AME_PFN(ame_sweep_workers_fit)(const ame_dims* dm, int mode) {
     switch (dm->r) {
 #define X(RR) \
-    case RR: return workers_fit<RR>(dm->n, dm->T_local) ? 1 : 0;
+    case RR: return (mode == 3 ? workers_fit<RR, 3>(dm->n, dm->T_local) \
+                               : workers_fit<RR, 2>(dm->n, dm->T_local)) ? 1 : 0;
         AME_FOR_EACH_R(X)
 #undef X
         default: return 0;

@@ -353,7 +353,9 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             // and slice t+1 cannot finish before slice t.  A larger value is stale
             // memory (a recycled buffer, a host write not yet ordered before this
             // launch): it sets AME_STATUS_STALE_EPOCH instead of being taken as done.
-            for (int q = 0; q < 2 && tl + q < TL; ++q) {
+            // (done[TL]: the next slice group's first slice, when one follows)
+            const int qn = (tl + 1 < TL || (a.flags & AME_SWEEP_FLAG_NEXT_GROUP)) ? 2 : 1;
+            for (int q = 0; q < qn; ++q) {
                 while (true) {
                     const uint32_t dv = __hip_atomic_load(a.done + tl + q, __ATOMIC_RELAXED,
                                                           __HIP_MEMORY_SCOPE_AGENT);

@@ -302,11 +302,24 @@ class DeviceEngine:
                 gd = _lib.ame_dims(self.n, self.r, w, sh.t_begin, sh.T_total, self.vcode)
                 if int(self.L.ame_sweep_kind(ctypes.byref(gd), req)) == _lib.AME_SWEEP_V2_WORKERS:
                     self.max_slices = w
-        self.groups = slice_groups(sh.T_local, self.max_slices, opt.slice_group)
+        # Pipelined layout: a kernel that orders itself slice by slice on the
+        # device (done flags) runs with TWO launches co-resident -- consecutive
+        # sweeps, and consecutive slice groups of one sweep -- so each launch gets
+        # at most half of what co-resides; the launches alternate over two
+        # streams
+        pipe_cap = 0
+        if opt.pipeline and self.max_slices >= 2:
+            half = self.max_slices // 2
+            pd = _lib.ame_dims(self.n, self.r, max(1, min(sh.T_local, half)), sh.t_begin,
+                               sh.T_total, self.vcode)
+            pk = int(self.L.ame_sweep_kind(ctypes.byref(pd), req))
+            if pk >= 0 and bool(self.L.ame_sweep_orders_slices(self.n, self.r, pk)):
+                pipe_cap = half
+        self.groups = slice_groups(sh.T_local, pipe_cap or self.max_slices, opt.slice_group)
         # the kernel of each group size is resolved ONCE here and passed with
         # every launch (ame_sweep rejects a launch whose buffers were sized for
-        # another kind); the groups of a sweep run one after another and share
-        # the scratch
+        # another kind); groups that run one after another share the scratch,
+        # pipelined launches alternate between two halves of it
         self.group_kinds = {}
         sws = 1
         for size in sorted({sz for _, sz in self.groups}):
@@ -319,22 +332,23 @@ class DeviceEngine:
                 _lib.check(-1, "ame_sweep_work_size")
             self.group_kinds[size] = k
             sws = max(sws, w)
-        self.sweep_work = torch.empty(sws, dtype=torch.float64, device=dev)
         self.sweep_kind = self.group_kinds[self.groups[0][1]]
         self._out_host = None
         self._out_valid = False
         self.timing = False       # record HIP events around each kernel launch
         self.events = []          # (name, start, end) while timing
         self.speculation = bool(opt.speculate)
-        self._specs = collections.deque()   # (done-event, ring slot) of sweeps started ahead
-        # consecutive sweeps alternate between two high-priority streams
+        self._specs = collections.deque()   # (done events, ring slot) of sweeps started ahead
+        # consecutive sweeps (or, pipelined, consecutive launches) alternate
+        # between two high-priority streams
         self.sweep_streams = [torch.cuda.Stream(device=self.dev, priority=-1) for _ in range(2)]
+        self._launch_ctr = 0
         self.done = torch.zeros(max(sh.T_local, 1), dtype=torch.int32, device=self.dev)
         kinds = set(self.group_kinds.values())
-        self.pipelined = (len(kinds) == 1
+        self.pipelined = (len(kinds) == 1 and pipe_cap > 0
                           and bool(self.L.ame_sweep_orders_slices(self.n, self.r, self.sweep_kind))
-                          and len(self.groups) == 1
-                          and 2 * sh.T_local <= self.max_slices
+                          and 2 * max(sz for _, sz in self.groups)
+                          <= int(self.L.ame_sweep_max_slices(self.n, self.r, self.sweep_kind))
                           and bool(opt.pipeline))
         if self.halo is not None:   # every rank must take the same path
             self.pipelined = self.halo.agree(self, self.pipelined)
@@ -355,7 +369,11 @@ class DeviceEngine:
             # with more than one queued that is a serial chain anyway, so the
             # queue is one deep (_launch_sweep also orders after the last one).
             self.spec_depth = 1
+        # scratch per launch; pipelined, two launches run at once: two halves
+        self._work_half = sws
         with torch.cuda.device(dev):
+            self.sweep_work = torch.empty(sws * (2 if self.pipelined else 1), dtype=torch.float64,
+                                          device=dev)
             while len(self.xs) < self.spec_depth + 1:
                 self.xs.append(torch.empty_like(self.xs[0]))
                 self.covs.append(torch.empty_like(self.covs[0]))
@@ -397,11 +415,11 @@ class DeviceEngine:
         e.record(s)
         return (name, e, s)
 
-    def _toc(self, tok):
+    def _toc(self, tok, stream=None):
         if tok is None:
             return
         e = torch.cuda.Event(enable_timing=True)
-        e.record(tok[2])
+        e.record(tok[2] if stream is None else stream)
         self.events.append((tok[0], tok[1], e))
 
     def kernel_ms(self):
@@ -436,19 +454,18 @@ class DeviceEngine:
     def _launch_sweep(self, spec=False):
         """Enqueue one sweep from the newest state (the last queued sweep's
         output, or the current state) into the next ring slot; returns
-        (done-event, slot).
+        (done-events, slot).
         A speculative sweep in pipelined mode is queued while the previous sweep
         (epoch - 1) still runs and orders itself slice by slice on the device;
-        any other sweep is ordered after everything queued on the main stream."""
+        any other sweep is ordered after everything queued on the main stream.
+        Pipelined engines alternate their launches -- sweeps and slice groups --
+        over the two sweep streams, so launch j + 1 runs beside launch j and
+        launch j + 2 queues behind launch j (at most two co-resident); otherwise
+        a sweep's groups run in order on one stream."""
         src = self._specs[-1][1] if self._specs else self._cur
         dst = (src + 1) % len(self.xs)
         self.epoch += 1
         _note_epoch(self.epoch)
-        # two streams: sweep k+2 queues behind sweep k's local slices, which keeps
-        # the launch-order XCD placement of its workgroups (three streams, measured:
-        # 16 % slower per iteration at n=128); the host-side constraint a deeper
-        # queue lifts is global (DESIGN.md §5)
-        stream = self.sweep_streams[self.epoch & 1]
         pipe = spec and self.pipelined and self.speculation
         halo_in = halo_out = next_old = back_in = back_out = None
         if self.halo is not None:
@@ -457,21 +474,41 @@ class DeviceEngine:
             next_old, halo_in, halo_out = self.halo.before_sweep(
                 self, gather=not pipe, first=self.xs[src][0])
             back_in, back_out = self.halo.back_channels(self)
-        wait = 0
-        if pipe:
-            wait = self.epoch - 1
-            if self._order_after_host_writes:
-                stream.wait_event(self._host_ready)
-        else:
+        wait = self.epoch - 1 if pipe else 0
+        ready = None
+        if not pipe:
             ready = torch.cuda.Event()
             ready.record(self.stream)
-            stream.wait_event(ready)
-            if self._specs:   # its input slot is the output of the last queued sweep
-                stream.wait_event(self._specs[-1][0])
-        tok = self._tic("sweep", stream)
+        prev = self._specs[-1][0] if self._specs else []
+        used = []
+
+        def order(stream):   # first launch of this sweep on `stream`
+            if stream in used:
+                return
+            used.append(stream)
+            if pipe:
+                if self._order_after_host_writes:
+                    stream.wait_event(self._host_ready)
+            else:
+                stream.wait_event(ready)
+                for ev in prev:   # its input slot is the output of the last queued sweep
+                    stream.wait_event(ev)
+
+        tok = None
         n, d, sh = self.n, self.d, self.shard
         last = len(self.groups) - 1
+        stream = None
         for g, (off, size) in enumerate(self.groups):
+            if self.pipelined:
+                par = self._launch_ctr & 1
+                self._launch_ctr += 1
+            else:
+                par = 0
+            stream = self.sweep_streams[par if self.pipelined else (self.epoch & 1)]
+            order(stream)
+            if tok is None:
+                tok = self._tic("sweep", stream)
+
             def at(t, slices, per_slice, esize):   # pointer to local slice `slices` of t
                 return ctypes.c_void_p(t.data_ptr() + slices * per_slice * esize)
             nd, ndd, nn2 = n * d, n * d * d, n * self.ny * 2
@@ -480,27 +517,32 @@ class DeviceEngine:
             g_next_old = next_old if g == last else at(self.xs[src], off + size, nd, 4)
             dims = _lib.ame_dims(n, self.r, size, sh.t_begin + off, sh.T_total, self.vcode)
             a = _lib.ame_sweep_args(
-                kind=self.group_kinds[size], work_doubles=self.sweep_work.numel(),
+                kind=self.group_kinds[size], work_doubles=self._work_half,
                 Yt=at(self.Yt, off, nn2, 4), x_old=at(self.xs[src], off, nd, 4),
                 x_new=at(self.xs[dst], off, nd, 4), next_old=g_next_old,
                 hand=at(self.hand, off, nd, 8), halo_in=g_halo_in, halo_out=g_halo_out,
                 cov=at(self.covs[src], off, ndd, 4), consts=_ptr(self.consts),
                 rinv=self.C.rinv4(), lr=self.lr, one_minus_lr=float(1.0 - self.lr),
-                epoch=self.epoch, status=_ptr(self.status), work=_ptr(self.sweep_work),
+                epoch=self.epoch, status=_ptr(self.status),
+                work=at(self.sweep_work, par, self._work_half, 8),
                 cov_new=at(self.covs[dst], off, ndd, 4), done=at(self.done, off, 1, 4),
                 wait_epoch=wait, back_out=back_out if g == 0 else None,
-                back_in=back_in if g == last else None)
+                back_in=back_in if g == last else None,
+                flags=_lib.AME_SWEEP_FLAG_NEXT_GROUP if g < last else 0)
             _lib.check(self.L.ame_sweep(ctypes.byref(dims), ctypes.byref(a),
                                         ctypes.c_void_p(stream.cuda_stream)), "ame_sweep")
-        self._toc(tok)
-        # the kernels take raw pointers: tell the caching allocator this stream
-        # uses the buffers, so a dropped engine's memory is not handed out again
+        self._toc(tok, stream)
+        # the kernels take raw pointers: tell the caching allocator these streams
+        # use the buffers, so a dropped engine's memory is not handed out again
         # while a sweep still reads or writes it
-        for t in (self.xs[src], self.xs[dst], self.covs[src], self.covs[dst], self.hand,
-                  self.done, self.status, self.sweep_work, self.Yt, self.consts):
-            t.record_stream(stream)
-        done = torch.cuda.Event()
-        done.record(stream)
+        done = []
+        for st in used:
+            for t in (self.xs[src], self.xs[dst], self.covs[src], self.covs[dst], self.hand,
+                      self.done, self.status, self.sweep_work, self.Yt, self.consts):
+                t.record_stream(st)
+            ev = torch.cuda.Event()
+            ev.record(st)
+            done.append(ev)
         return done, dst
 
     def _commit(self, slot):
@@ -515,7 +557,8 @@ class DeviceEngine:
             done, slot = self._specs.popleft()
         else:
             done, slot = self._launch_sweep()
-        self.stream.wait_event(done)
+        for ev in done:
+            self.stream.wait_event(ev)
         self._commit(slot)
         if self.halo is not None:
             self.halo.after_sweep(self)
@@ -536,7 +579,8 @@ class DeviceEngine:
         spare ring slots; later main-stream work is ordered after them."""
         while self._specs:
             done, _ = self._specs.popleft()
-            self.stream.wait_event(done)
+            for ev in done:
+                self.stream.wait_event(ev)
 
     def refresh_cov_terms(self):
         """Covariance ELBO terms of the current covariances (no update)."""

@@ -32,12 +32,17 @@ def _free_port():
     return p
 
 
+V3, W22, P23 = 3, 22, 23   # _lib.AME_SWEEP_V3, _lib.AME_SWEEP_V2_WORKERS, _lib.AME_SWEEP_V2_PIPE
+
+
 def _run(n, T, r, method, lr, iters, distributed, depth=None, kind=None):
     from ame_amd import TemporalAMEModel, TemporalAMENaiveMFVI, TemporalAMEStructuredMFVI
     m = TemporalAMEModel(n, T, r, seed=21)
     m.generate_data_fast(seed=4)
     dev = torch.device("cuda", 0)
     opts = {} if depth is None else {"spec_depth": depth}
+    if kind == P23:   # requested: AUTO picks kind 22 for these shapes
+        opts["sweep_kernel"] = P23
     if method == "naive":
         vi = TemporalAMENaiveMFVI(m, learning_rate=lr, device=dev, distributed=distributed,
                                   engine_options=opts)
@@ -68,9 +73,6 @@ def _worker(rank, world, port, args, q):
         dist.destroy_process_group()
 
 
-V3, W22 = 3, 22   # _lib.AME_SWEEP_V3, _lib.AME_SWEEP_V2_WORKERS
-
-
 @pytest.mark.parametrize("world,n,T,r,method,lr,iters,depth,kind", [
     (2, 64, 8, 4, "good", 0.5, 3, None, V3), (2, 40, 6, 3, "bad", 1.0, 3, None, V3),
     (2, 48, 5, 2, "naive", 0.3, 3, None, V3), (3, 50, 9, 3, "good", 0.5, 6, None, V3),
@@ -83,7 +85,11 @@ V3, W22 = 3, 22   # _lib.AME_SWEEP_V3, _lib.AME_SWEEP_V2_WORKERS
     # the workers' partial ring, 2 and 3 ranks, good / bad / naive, in-order
     # sweeps over several iterations (kind 22 does not pipeline)
     (2, 300, 8, 32, "good", 0.5, 3, None, W22), (3, 240, 12, 32, "bad", 0.7, 3, None, W22),
-    (2, 200, 6, 32, "naive", 0.4, 4, None, W22), (3, 301, 9, 32, "good", 0.01, 3, None, W22)])
+    (2, 200, 6, 32, "naive", 0.4, 4, None, W22), (3, 301, 9, 32, "good", 0.01, 3, None, W22),
+    # the pipelined GEMV-worker sweep (kind 23) across ranks: pipelined sweeps,
+    # back channels and halo granules between ranks, depth 2 and 3
+    (2, 300, 8, 32, "good", 0.5, 5, None, P23), (3, 240, 12, 32, "bad", 0.7, 6, 3, P23),
+    (2, 200, 6, 32, "naive", 0.4, 5, None, P23)])
 def test_ranks_one_gpu(world, n, T, r, method, lr, iters, depth, kind):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")

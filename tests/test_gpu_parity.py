@@ -357,6 +357,8 @@ def test_slice_groups_are_exact(group, gpu_device):
         m.generate_data_fast(seed=12)
         vi = _vi(m, "good", 0.5, gpu_device, slice_group=g)
         assert len(vi.engine.groups) == (1 if g == 0 else -(-10 // g))
+        # groups of a pipelined kernel alternate streams and overlap on the device
+        assert vi.engine.pipelined
         h = vi.fit(max_iter=3, tolerance=0.0, verbose=False)
         outs.append((vi.X_mean.numpy().copy(), vi.X_cov.numpy().copy(), [float(e) for e in h["elbo"]]))
     assert np.array_equal(outs[0][0], outs[1][0])
