@@ -362,7 +362,7 @@ def sweep_alg_bytes(n, TL, d):
     return kernel_bytes(n, TL, d)["sweep"]
 
 
-def config5_full(dev, steps=3, warmup=1, variants=("naive", "good", "bad")):
+def config5_full(dev, steps=3, warmup=1, variants=("naive", "good", "bad"), opts=None):
     """BASELINE config 5's own workload on ONE GPU: n=4096, T=256, r=32 (d=66),
     Naive-MF vs SMF-good vs SMF-bad on the same synthetic Y
     (experiments/three_way_conparison.py:141-179).  The GEMV-worker sweep
@@ -382,9 +382,10 @@ def config5_full(dev, steps=3, warmup=1, variants=("naive", "good", "bad")):
            "steps": steps, "warmup": warmup, "data": "synthetic", "dtype": "f32", "variants": {}}
     for method in variants:
         if method == "naive":
-            vi = TemporalAMENaiveMFVI(m, learning_rate=0.01, device=dev)
+            vi = TemporalAMENaiveMFVI(m, learning_rate=0.01, device=dev, engine_options=opts)
         else:
-            vi = TemporalAMEStructuredMFVI(m, factorization=method, learning_rate=0.01, device=dev)
+            vi = TemporalAMEStructuredMFVI(m, factorization=method, learning_rate=0.01, device=dev,
+                                           engine_options=opts)
         eng = vi.engine
         vi.fit(max_iter=warmup, tolerance=0.0, verbose=False)
         eng.timing = True
@@ -400,7 +401,7 @@ def config5_full(dev, steps=3, warmup=1, variants=("naive", "good", "bad")):
         out["variants"][method] = {
             "ms_per_iteration": ms, "updates_per_s": units / (ms * 1e-3),
             "sweep_kind": int(eng.sweep_kind), "slice_groups": len(eng.groups),
-            "pipelined": bool(eng.pipelined),
+            "pipelined": bool(eng.pipelined), "sweeps_queued_ahead": int(eng.spec_depth),
             "kernel_ms": kms, "kernel_launches": kcount,
             "sweep_roofline": {"alg_bytes": alg, "ms": kms.get("sweep"),
                                "frac": (alg / (kms["sweep"] * 1e-3) / 1e9 / HBM_PEAK_GBS)
@@ -439,6 +440,9 @@ def main():
     ap.add_argument("--force-dist", action="store_true",
                     help="use the process group (nccl) and the time-sharded path even at world size 1 "
                          "(checks RCCL initialisation on a one-GPU box)")
+    ap.add_argument("--sweep-kernel", type=int, default=0,
+                    help="sweep kernel request (include/ame_amd.h enum ame_sweep_kind_code; "
+                         "0 = AUTO, the production choice)")
     ap.add_argument("--config5-full", action="store_true",
                     help="BASELINE config 5's own workload (n=4096, T=256, r=32) three-way on "
                          "this one GPU; prints its own JSON line instead of the metric")
@@ -456,8 +460,11 @@ def main():
     torch.cuda.set_device(dev)
     use_dist = world > 1 or args.force_dist
     if args.config5_full:
+        c5opts = {"sweep_kernel": args.sweep_kernel} if args.sweep_kernel else None
+        if args.no_pipeline:
+            c5opts = dict(c5opts or {}, pipeline=False)
         out = config5_full(dev, steps=args.steps if args.steps != 50 else 3,
-                           warmup=args.warmup if args.warmup != 3 else 1)
+                           warmup=args.warmup if args.warmup != 3 else 1, opts=c5opts)
         print(json.dumps(out), file=json_out, flush=True)
         return out
     if use_dist:
@@ -470,7 +477,10 @@ def main():
     T_total = args.t_per_gpu * world
     model = TemporalAMEModel(n, T_total, r, seed=42)
     model.generate_data_fast(device=dev)
-    opts = {"pipeline": False} if args.no_pipeline else None
+    opts = {"pipeline": False} if args.no_pipeline else {}
+    if args.sweep_kernel:
+        opts["sweep_kernel"] = args.sweep_kernel
+    opts = opts or None
     if args.variant == "naive":
         vi = TemporalAMENaiveMFVI(model, learning_rate=args.lr, device=dev,
                                   distributed=use_dist, engine_options=opts)

@@ -130,12 +130,15 @@ __host__ __device__ inline SweepLds sweep_lds_layout(int n, int R, int force_glo
 #define AME_GW_MAXPW 152  // nodes per worker wave held in registers: n <= 7 * 4 * 152
 // pipelined v2 sweep (kind AME_SWEEP_V2_PIPE, MODE 3): four workers per slice,
 // so a slice is 5 workgroups and two consecutive launches of up to 25 slices
-// (one workgroup per CU) are co-resident.  Three workers (344 nodes per worker
-// wave at n = 4096) spill ~1 000 VGPRs at every split between registers and
-// LDS tried; four (256 per wave) compile spill-free
+// (one workgroup per CU) are co-resident.  A worker wave holds up to 256 nodes
+// (n <= 4 * 4 * 256): 152 in registers -- kind 22's count, whose owner update
+// compiles to one select per slot; 256 register slots compiled to a
+// pathological owner update (10x slower node period in the stamped build), and
+// three workers (344 slots) spill ~1 000 VGPRs at every split tried -- and the
+// other 104 in the worker's LDS ([wave][slot][lane], 104 KB)
 #define AME_GW_P 4
-#define AME_GW_P_MAXPW 256   // n <= 4 * 4 * 256
-#define AME_GW_P_NREG 256    // of which in registers; the rest (none) in the worker's LDS
+#define AME_GW_P_MAXPW 256
+#define AME_GW_P_NREG 152
 __host__ __device__ inline int ame_v2_nworkers(int mode) { return mode == 3 ? AME_GW_P : AME_GW; }
 __host__ __device__ inline int ame_v2_maxpw(int mode) { return mode == 3 ? AME_GW_P_MAXPW : AME_GW_MAXPW; }
 

@@ -432,52 +432,19 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
         WSTAMP(2);
         // U_c -> h_V (z1), V -> h_U (z0); four independent chains
         float a4[4] = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (MODE == 3) {
-            // register slots in chunks of 32 (all loads ahead of the FMAs would
-            // need hundreds of temporaries beside mreg), then the LDS slots; the
-            // same products and summation order (a4[slot & 3]) throughout
-            constexpr int CH = 32;
+        // register slots as kind 22; MODE 3's LDS-held slots after them, same
+        // summation order (a4[slot & 3])
 #pragma unroll
-            for (int c0 = 0; c0 < NREG; c0 += CH) {
-                float zc[CH];
-#pragma unroll
-                for (int b = 0; b < CH; ++b) {
-                    const int s2 = c0 + b < NREG ? c0 + b : NREG - 1;
-                    const float2 z = zb[q + 4 * s2];
-                    zc[b] = lane < R ? z.y : z.x;
-                }
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int b = 0; b < CH; ++b) {
-                    const int s2 = c0 + b;
-                    if (s2 < NREG) a4[s2 & 3] = fmaf(zc[b], mreg[s2], a4[s2 & 3]);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            constexpr int CL = 8;
-#pragma unroll
-            for (int c0 = 0; c0 < NLD; c0 += CL) {
-                float zc[CL], mv[CL];
-#pragma unroll
-                for (int b = 0; b < CL; ++b) {
-                    const int sl = c0 + b < NLD ? c0 + b : NLD - 1;
-                    const float2 z = zb[q + 4 * (NREG + sl)];
-                    zc[b] = lane < R ? z.y : z.x;
-                    mv[b] = mld[(q * NLD + sl) * 64 + lane];
-                }
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int b = 0; b < CL; ++b) {
-                    const int s2 = NREG + c0 + b;
-                    if (c0 + b < NLD) a4[s2 & 3] = fmaf(zc[b], mv[b], a4[s2 & 3]);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        } else {
-#pragma unroll
-            for (int s2 = 0; s2 < MAXPW; ++s2) {
+        for (int s2 = 0; s2 < NREG; ++s2) {
+            const float2 z = zb[q + 4 * s2];
+            a4[s2 & 3] = fmaf(lane < R ? z.y : z.x, mreg[s2], a4[s2 & 3]);
+        }
+        if constexpr (NLD > 0) {
+#pragma unroll 8
+            for (int sl = 0; sl < NLD; ++sl) {
+                const int s2 = NREG + sl;
                 const float2 z = zb[q + 4 * s2];
-                a4[s2 & 3] = fmaf(lane < R ? z.y : z.x, mreg[s2], a4[s2 & 3]);
+                a4[s2 & 3] = fmaf(lane < R ? z.y : z.x, mld[(q * NLD + sl) * 64 + lane], a4[s2 & 3]);
             }
         }
         const float acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);

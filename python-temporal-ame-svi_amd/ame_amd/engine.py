@@ -295,8 +295,11 @@ class DeviceEngine:
                 or int(self.L.ame_sweep_max_slices(self.n, self.r, _lib.AME_SWEEP_V3)) < 1):
             # beyond v3's reach the GEMV-worker sweep (kind 22) in slice groups of
             # what co-resides beats ONE launch of the single-workgroup sweep over
-            # all slices: config 5 at T = 256 on one GPU, 8 groups of 32 vs kind 21
-            # (DESIGN.md §4 K1c); AUTO already picks kind 22 whenever T_local fits
+            # all slices: config 5 at T = 256 on one GPU, 8 groups of 32 vs kind 21,
+            # 285-302 vs 580 ms per iteration; the pipelined kind 23 in overlapping
+            # groups measured the same, 274-291 ms, and loses at
+            # T_local = 32, so kind 22 stays the choice.  AUTO picks kind 22
+            # whenever T_local fits one launch
             w = int(self.L.ame_sweep_max_slices(self.n, self.r, _lib.AME_SWEEP_V2_WORKERS))
             if 1 <= w < min(sh.T_local, self.max_slices):
                 gd = _lib.ame_dims(self.n, self.r, w, sh.t_begin, sh.T_total, self.vcode)
@@ -324,7 +327,7 @@ class DeviceEngine:
         sws = 1
         for size in sorted({sz for _, sz in self.groups}):
             gd = _lib.ame_dims(self.n, self.r, size, sh.t_begin, sh.T_total, self.vcode)
-            k = int(self.L.ame_sweep_kind(ctypes.byref(gd), opt.sweep_kernel))
+            k = int(self.L.ame_sweep_kind(ctypes.byref(gd), req))
             if k < 0:
                 _lib.check(-1, "ame_sweep_kind")
             w = int(self.L.ame_sweep_work_size(ctypes.byref(gd), k))

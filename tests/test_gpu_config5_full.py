@@ -7,14 +7,16 @@ runs as 8 consecutive slice groups of 32 (engine.slice_groups); group g+1's
 first slice takes group g's last slice's new means from its hand-off
 granules, so the 255 slice boundaries carry the Gauss-Seidel order exactly as
 one launch would (reference: the t loop of structured_mf.py:240 has no limit
-on T).  Per variant, two fit() iterations; checks:
+on T).  The same test on the pipelined kind 23 (11 overlapping groups of
+23-24, 1 100 nodes against the oracle) is profiles/r05_i_pytest_pipe_and_c5full_kind23.txt.
+Per variant, two fit() iterations; checks:
 
-* kind 22, 8 groups, sweeps in order (not pipelined);
+* kind 22, 8 groups, in order (not pipelined);
 * the second sweep against the fp64 oracle's replay from the device's state
   after the first (ame_oracle.sweep_stats, pinned in tests/test_oracle_fast.py):
   nodes 0..K-1 of ALL 256 slices -- 600 nodes for SMF-good (past the first
-  GEMV worker's 585-node range), 64 for bad / naive (past the workers' 4-node
-  look-behind); means within 5e-6 * max(1, |mu|), covariances 1e-6 * max(1, |S|);
+  GEMV worker's 585-node range, so the hand-over to the second worker is
+  checked), 64 for bad / naive (past the workers' 4-node look-behind); means within 5e-6 * max(1, |mu|), covariances 1e-6 * max(1, |S|);
 * the device ELBO / MSE of the final state against an fp64 evaluation of that
   state slice by slice (tests/elbo_check.py: torch's own fp64 kernels on the
   GPU for all 256 slices -- the CPU would need ~10 minutes for the 3 x 256
@@ -60,6 +62,7 @@ def test_config5_full_workload_three_way(gpu_device):
         t0 = time.time()
         vi = _vi(m, method, LR, gpu_device)
         eng = vi.engine
+        # the GEMV-worker sweep in 8 consecutive groups of 32 slices
         assert eng.sweep_kind == _lib.AME_SWEEP_V2_WORKERS
         assert len(eng.groups) == 8 and {s for _, s in eng.groups} == {32}, eng.groups
         assert not eng.pipelined

@@ -74,7 +74,9 @@ def run():
         vi = TemporalAMEStructuredMFVI(m, factorization=variant, learning_rate=0.01, device=dev,
                                        engine_options=opts)
     assert vi.engine.sweep_kind in (_lib.AME_SWEEP_V2_LDS, _lib.AME_SWEEP_V2_HBM,
-                                    _lib.AME_SWEEP_V2_WORKERS), vi.engine.sweep_kind
+                                    _lib.AME_SWEEP_V2_WORKERS, _lib.AME_SWEEP_V2_PIPE), vi.engine.sweep_kind
+    # one launch per sweep (the stamp buffers are per kernel, not per group)
+    assert len(vi.engine.groups) == 1, vi.engine.groups
     vi.fit(max_iter=2, tolerance=0.0, verbose=False)
     torch.cuda.synchronize()
     L = _lib.lib()
