@@ -137,8 +137,12 @@ __host__ __device__ inline SweepLds sweep_lds_layout(int n, int R, int force_glo
 // three workers (344 slots) spill ~1 000 VGPRs at every split tried -- and the
 // other 104 in the worker's LDS ([wave][slot][lane], 104 KB)
 #define AME_GW_P 4
+#ifndef AME_GW_P_MAXPW       // (variant builds for A/B runs may override both)
 #define AME_GW_P_MAXPW 256
+#endif
+#ifndef AME_GW_P_NREG
 #define AME_GW_P_NREG 152
+#endif
 __host__ __device__ inline int ame_v2_nworkers(int mode) { return mode == 3 ? AME_GW_P : AME_GW; }
 __host__ __device__ inline int ame_v2_maxpw(int mode) { return mode == 3 ? AME_GW_P_MAXPW : AME_GW_MAXPW; }
 

@@ -195,6 +195,24 @@ struct ArPart {
     static constexpr int MC = (D + NPA - 1) / NPA;
 };
 
+// mreg[sn] = val for a wave-uniform runtime slot index sn: a binary search of
+// uniform branches down to a compile-time index (log2(N) scalar compares and
+// one write) instead of a select on every slot -- the registers may live in
+// AGPRs, where each select costs a read, a cndmask and a write
+template <int LO, int HI, int N>
+__device__ __forceinline__ void set_slot(float (&mreg)[N], int sn, float val, bool col) {
+    if constexpr (HI - LO == 1) {
+        if (col) mreg[LO] = val;
+        // opaque per leaf: otherwise the leaves' stores merge into one store at a
+        // runtime index, which demotes mreg to scratch memory
+        asm volatile("" : "+v"(mreg[LO]));
+    } else {
+        constexpr int MID = (LO + HI) / 2;
+        if (sn < MID) set_slot<LO, MID, N>(mreg, sn, val, col);
+        else set_slot<MID, HI, N>(mreg, sn, val, col);
+    }
+}
+
 // Pipelined launch (MODE 3, wait_epoch != 0): every workgroup of slice t -- the
 // slice's own and its GEMV workers -- reads the previous sweep's outputs for
 // slices t and t+1 (old means, covariances; slice t+1 also reads the hand-off
@@ -406,10 +424,9 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
                 }
             }
             const float val = __uint_as_float((uint32_t)v);
-#pragma unroll
-            for (int s2 = 0; s2 < NREG; ++s2)
-                if (s2 == sn && col) mreg[s2] = val;
-            if (NLD > 0 && sn >= NREG && col) mld[(q * NLD + (sn - NREG)) * 64 + lane] = val;
+            const int snu = __builtin_amdgcn_readfirstlane(sn);   // wave-uniform (owner wave)
+            if (snu >= 0 && snu < NREG) set_slot<0, NREG, NREG>(mreg, snu, val, col);
+            if (NLD > 0 && snu >= NREG && col) mld[(q * NLD + (snu - NREG)) * 64 + lane] = val;
         }
         WSTAMP(1);
         // z row of node m over the range (nodes m-3..m left out)
@@ -440,8 +457,10 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
             a4[s2 & 3] = fmaf(lane < R ? z.y : z.x, mreg[s2], a4[s2 & 3]);
         }
         if constexpr (NLD > 0) {
+            // only the LDS slots that hold nodes (none below n = 4 * 4 * NREG)
+            const int nlv = min(NLD, max(0, npw - NREG));
 #pragma unroll 8
-            for (int sl = 0; sl < NLD; ++sl) {
+            for (int sl = 0; sl < nlv; ++sl) {
                 const int s2 = NREG + sl;
                 const float2 z = zb[q + 4 * s2];
                 a4[s2 & 3] = fmaf(lane < R ? z.y : z.x, mld[(q * NLD + sl) * 64 + lane], a4[s2 & 3]);
