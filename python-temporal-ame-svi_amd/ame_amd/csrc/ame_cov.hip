@@ -31,6 +31,8 @@
 // The input is taken as symmetric: the sweep writes symmetric covariances and
 // the reference's initialisation symmetrises (structured_mf.py:94-96).
 #include "ame_common.h"
+#include "ame_wave.h"
+#include <type_traits>
 
 template <int R>
 struct CovCfg {
@@ -220,8 +222,294 @@ ame_cov_kernel(ame_dims dm, ame_cov_args a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// MFMA form (r >= AME_COV_MFMA_MIN_R).  Why: the column-per-lane form above
+// delivers the pivot row to every lane through LDS -- one 8-byte LDS return
+// per FMA, ~1 MB of LDS data per 64 x 64 complement -- and at r = 32 that is
+// its bound (1.9 ms at config 5's rank shape, 0.15 of HBM).  Here one wave
+// owns one covariance and keeps the 2r x 2r complement as the lower 16 x 16
+// tiles of v_mfma_f64_16x16x4_f64's accumulator layout (lane l, register v:
+// row (l >> 4) + 4 v, column l & 15), padded to a multiple of 16 with the
+// identity (pivots 1: no change to log|S|).  Right-looking blocked LDL^T in
+// panels of 4 columns:
+//  a) the panel's 4 columns (rows >= 16 J_p) leave the tiles through LDS into
+//     row-per-lane form (lane r: row r; rows above the panel zeroed);
+//  b) its 4 pivots eliminate inside the panel, the pivot row by v_readlane;
+//  c) every trailing tile takes the panel's rank-4 update as ONE MFMA (K = 4):
+//     S_IJ -= (W_I diag(1/piv)) W_J^T, operands read back column-major (lane
+//     (i, k) holds W[16 I + i][k]).
+// Tile entries left of / above the trailing block are updated as well and
+// never read again (each panel leaves the tiles before its update).  The
+// (a,b) block's Schur correction S = A22 - U A_aa^-1 U^T is one MFMA per tile
+// too (K = 2 of 4, the other operand lanes zero).  Traces come from the
+// loaded entries with per-lane weights (tiles below the diagonal count their
+// mirror: M symmetric), Q^-1's from LDS, S0^-1's (slice 0 only) from global.
+// LDS carries ~60 KB per 64 x 64 covariance instead of ~1 MB.
+// ---------------------------------------------------------------------------
+#ifndef AME_COV_MFMA_MIN_R
+#define AME_COV_MFMA_MIN_R 20
+#endif
+typedef double ame_d4 __attribute__((ext_vector_type(4)));
+
+template <int R>
+struct CovM {
+    static constexpr int B = 2 * R, D = B + 2, DD = D * D;
+    static constexpr int NT = (B + 15) / 16;          // tiles per dimension
+    static constexpr int BP = 16 * NT;                // padded complement
+    static constexpr int NTL = NT * (NT + 1) / 2;     // lower tiles, I >= J
+    static constexpr int NWT = 4 * NTL + 2 * NT;      // trace weights per lane
+    static constexpr int WPB = 4;                     // waves per block
+};
+__host__ __device__ constexpr int cov_ti(int I, int J) { return I * (I + 1) / 2 + J; }
+
+// weight of this lane's loaded entry `pos` in tr(M A), M symmetric: entries
+// 0 .. 4 NTL-1 are tile registers (below-diagonal tiles stand for their mirror
+// as well), then the (a,b)-column pairs of rows 16 I + (lane & 15) (counted on
+// lanes 0..15, for A[k][0..1] and A[0..1][k])
+template <int R>
+__device__ __forceinline__ double cov_mweight(const double* M, int pos, int lane) {
+    using C = CovM<R>;
+    if (pos < 4 * C::NTL) {
+        const int t = pos >> 2, v = pos & 3;
+        int I = 0;
+        while ((I + 1) * (I + 2) / 2 <= t) ++I;
+        const int J = t - I * (I + 1) / 2;
+        const int row = 16 * I + (lane >> 4) + 4 * v, col = 16 * J + (lane & 15);
+        if (row >= C::B || col >= C::B) return 0.0;
+        const double m = M[(2 + row) * C::D + 2 + col];
+        return I > J ? 2.0 * m : m;
+    }
+    const int q = pos - 4 * C::NTL, I = q >> 1, kk = q & 1;
+    const int row = 16 * I + (lane & 15);
+    if ((lane >> 4) != 0 || row >= C::B) return 0.0;
+    return 2.0 * M[kk * C::D + 2 + row];
+}
+
+template <int R, class WF>
+__device__ __forceinline__ double cov_mtrace(const ame_d4 (&tile)[CovM<R>::NTL], const float2 (&u)[CovM<R>::NT],
+                                             WF wf) {
+    using C = CovM<R>;
+    double tm = 0.0;
+#pragma unroll
+    for (int t = 0; t < C::NTL; ++t) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) tm = fma(wf(4 * t + v), tile[t][v], tm);
+    }
+#pragma unroll
+    for (int I = 0; I < C::NT; ++I) {
+        tm = fma(wf(4 * C::NTL + 2 * I), (double)u[I].x, tm);
+        tm = fma(wf(4 * C::NTL + 2 * I + 1), (double)u[I].y, tm);
+    }
+    return tm;
+}
+
+// Covariances [mc0, mc1) of the local block, all with the same trace matrix:
+// msel 0 = S0^-1 (slice 0), 1 = Q^-1 (the host splits the launch at slice 1)
+template <int R>
+__global__ void __launch_bounds__(256)
+ame_cov_mfma_kernel(ame_dims dm, ame_cov_args a, long long mc0, long long mc1, int msel) {
+    using C = CovM<R>;
+    constexpr int B = C::B, D = C::D, DD = C::DD, NT = C::NT, BP = C::BP, NTL = C::NTL, NWT = C::NWT,
+                  WPB = C::WPB;
+    __shared__ double wq[NWT * 64];                                  // trace weights [pos][lane]
+    __shared__ __attribute__((aligned(16))) double pbuf[WPB][64 * 4];   // per wave: the panel
+    // w uniform (readfirstlane): the covariance's base address stays in SGPRs and
+    // the tile loads take 32-bit lane offsets
+    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const double* M = a.consts + (msel ? DD : 0);
+    for (int e = tid; e < NWT * 64; e += 256) wq[e] = cov_mweight<R>(M, e >> 6, e & 63);
+    __syncthreads();
+    const double m00 = M[0], m01 = M[1], m10 = M[D], m11 = M[D + 1];
+    const long long stride = (long long)gridDim.x * WPB;
+    const int g = lane >> 4, c = lane & 15;
+    double* pb = pbuf[w];
+    for (long long mc = mc0 + (long long)blockIdx.x * WPB + w; mc < mc1; mc += stride) {
+        const float* A = a.cov + mc * DD;
+        const double a00 = A[0], a01 = A[1], a10 = A[D], a11 = A[D + 1];
+        float2 u[NT];   // A[2 + row][0..1], row = 16 I + c
+        float ft[NTL][4];   // tile entries as loaded (padding: the identity)
+#pragma unroll
+        for (int I = 0; I < NT; ++I) {
+            const int row = 16 * I + c;
+            u[I] = row < B ? *(const float2*)(A + (2 + row) * D) : make_float2(0.f, 0.f);
+        }
+#pragma unroll
+        for (int I = 0; I < NT; ++I)
+#pragma unroll
+            for (int J = 0; J <= I; ++J)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const int row = 16 * I + g + 4 * v, col = 16 * J + c;
+                    ft[cov_ti(I, J)][v] = (row < B && col < B) ? A[(2 + row) * D + 2 + col]
+                                                               : (row == col ? 1.f : 0.f);
+                }
+        // ---- traces, from the entries as loaded; the weights stream through
+        // (scheduling regions of two tiles: hoisted all at once, the 48 fp64
+        // weights held 96 VGPRs beside the tiles) ----
+        double tr = (lane == 0) ? a00 + a11 : 0.0;
+#pragma unroll
+        for (int I = 0; I < NT; ++I)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const int row = 16 * I + g + 4 * v;
+                if (row < B && g + 4 * v == c) tr += (double)ft[cov_ti(I, I)][v];
+            }
+        double tm = (lane == 0) ? m00 * a00 + m01 * a10 + m10 * a01 + m11 * a11 : 0.0;
+#pragma unroll
+        for (int I = 0; I < NT; ++I) {
+            tm = fma(wq[(4 * NTL + 2 * I) * 64 + lane], (double)u[I].x, tm);
+            tm = fma(wq[(4 * NTL + 2 * I + 1) * 64 + lane], (double)u[I].y, tm);
+        }
+#pragma unroll
+        for (int t = 0; t < NTL; ++t) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) tm = fma(wq[(4 * t + v) * 64 + lane], (double)ft[t][v], tm);
+            if (t & 1) asm volatile("" : "+v"(tm)::"memory");
+        }
+        // ---- Schur complement of the (a,b) block: S = A22 - U (A_aa^-1 U^T) ----
+        const double det2 = a00 * a11 - a01 * a10;
+        const double id2 = 1.0 / det2;
+        ame_d4 tile[NTL];
+        {
+            double ua[NT], wb[NT];
+#pragma unroll
+            for (int I = 0; I < NT; ++I) {
+                const double u0 = u[I].x, u1 = u[I].y;
+                const double w0 = (a11 * u0 - a01 * u1) * id2, w1 = (a00 * u1 - a10 * u0) * id2;
+                ua[I] = g == 0 ? -u0 : (g == 1 ? -u1 : 0.0);
+                wb[I] = g == 0 ? w0 : (g == 1 ? w1 : 0.0);
+            }
+#pragma unroll
+            for (int I = 0; I < NT; ++I)
+#pragma unroll
+                for (int J = 0; J <= I; ++J) {
+                    const int t = cov_ti(I, J);
+                    const ame_d4 a4 = {(double)ft[t][0], (double)ft[t][1], (double)ft[t][2], (double)ft[t][3]};
+                    tile[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ua[I], wb[J], a4, 0, 0, 0);
+                }
+        }
+        // ---- blocked LDL^T, panels of 4 columns ----
+        double prod = det2;
+        int e2 = 0, neg = det2 < 0.0 ? 1 : 0;
+        bool zero = det2 == 0.0;
+        // one tile column at a time (compile-time tile indices), its 4 panels in
+        // a loop (a full unroll let the compiler hoist across panels: 376 VGPRs)
+        auto tile_column = [&](auto JPc) {
+            constexpr int Jp = decltype(JPc)::value;
+#pragma unroll 1
+            for (int sub = 0; sub < 4; ++sub) {
+                const int p = 4 * Jp + sub, cb = 4 * sub;
+                // a) the panel's columns, rows >= 16 Jp, into LDS rows [r][k]
+                asm volatile("" ::: "memory");
+                if (c >= cb && c < cb + 4) {
+#pragma unroll
+                    for (int I = Jp; I < NT; ++I)
+#pragma unroll
+                        for (int v = 0; v < 4; ++v)
+                            pb[(16 * I + g + 4 * v) * 4 + (c - cb)] = tile[cov_ti(I, Jp)][v];
+                }
+                asm volatile("" ::: "memory");
+                const double2 x01 = *(const double2*)(pb + lane * 4);
+                const double2 x23 = *(const double2*)(pb + lane * 4 + 2);
+                const bool live = lane >= 4 * p && lane < BP;   // rows above the panel: zero
+                double x[4] = {live ? x01.x : 0.0, live ? x01.y : 0.0, live ? x23.x : 0.0, live ? x23.y : 0.0};
+                // b) the 4 pivots inside the panel
+                double rp[4];
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    const int P = 4 * p + kk;
+                    const double piv = ame::lane_bcast(x[kk], P);
+                    zero |= piv == 0.0;
+                    neg ^= piv < 0.0 ? 1 : 0;
+                    prod *= piv;
+                    if (kk == 3 && (sub & 1)) {   // every 8 pivots
+                        int ex;
+                        prod = frexp(prod, &ex);
+                        e2 += ex;
+                    }
+                    double ri = __builtin_amdgcn_rcp(piv);
+                    ri = fma(fma(-piv, ri, 1.0), ri, ri);
+                    ri = fma(fma(-piv, ri, 1.0), ri, ri);
+                    rp[kk] = ri;
+                    const double f = x[kk] * ri;
+#pragma unroll
+                    for (int kq = kk + 1; kq < 4; ++kq) x[kq] = fma(-ame::lane_bcast(x[kq], P), f, x[kq]);
+                }
+                // c) rank-4 update of the trailing tiles (J >= Jp, and J > Jp after
+                // the column's last panel), one MFMA each
+                if (Jp + 1 < NT || sub < 3) {
+                    asm volatile("" ::: "memory");
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk) pb[kk * 64 + lane] = x[kk];   // column-major [k][r]
+                    asm volatile("" ::: "memory");
+                    const double rk = g == 0 ? rp[0] : (g == 1 ? rp[1] : (g == 2 ? rp[2] : rp[3]));
+                    double xa[NT], xb[NT];
+#pragma unroll
+                    for (int I = Jp; I < NT; ++I) {
+                        xb[I] = pb[g * 64 + 16 * I + c];
+                        xa[I] = -xb[I] * rk;
+                    }
+#pragma unroll
+                    for (int I = Jp + 1; I < NT; ++I)
+#pragma unroll
+                        for (int J = Jp + 1; J <= I; ++J)
+                            tile[cov_ti(I, J)] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[I], xb[J], tile[cov_ti(I, J)], 0, 0, 0);
+                    if (sub < 3) {
+#pragma unroll
+                        for (int I = Jp; I < NT; ++I)
+                            tile[cov_ti(I, Jp)] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[I], xb[Jp], tile[cov_ti(I, Jp)], 0, 0, 0);
+                    }
+                }
+            }
+        };
+        static_assert(NT >= 1 && NT <= 4, "r <= 32");
+        tile_column(std::integral_constant<int, 0>{});
+        if constexpr (NT > 1) tile_column(std::integral_constant<int, 1>{});
+        if constexpr (NT > 2) tile_column(std::integral_constant<int, 2>{});
+        if constexpr (NT > 3) tile_column(std::integral_constant<int, 3>{});
+        double ld = log(fabs(prod)) + (double)e2 * 0.69314718055994530942;
+        if (zero) ld = -INFINITY;
+        else if (neg) ld = NAN;
+        tr = wave_sum(tr);
+        tm = wave_sum(tm);
+        if (lane == 0) {
+            double* o = a.cov_terms + mc * 4;
+            o[0] = ld;
+            o[1] = tr;
+            o[2] = msel ? tm : 0.0;
+            o[3] = msel ? 0.0 : tm;
+        }
+    }
+}
+
+template <int R>
+static int launch_cov_mfma(const ame_dims* dm, const ame_cov_args* a, hipStream_t st) {
+    using C = CovM<R>;
+    const long long total = (long long)dm->T_local * dm->n;
+    int dev = 0, cus = 0, per_cu = 0;
+    long long cap = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ame_cov_mfma_kernel<R>, 256, 0) == hipSuccess &&
+        cus > 0 && per_cu > 0)
+        cap = (long long)cus * per_cu;
+    // slice 0 (S0^-1) and the rest (Q^-1) as two launches
+    const long long split = (dm->t_begin == 0) ? (total < dm->n ? total : (long long)dm->n) : 0;
+    const long long lo[2] = {0, split}, hi[2] = {split, total};
+    for (int q = 0; q < 2; ++q) {
+        if (hi[q] <= lo[q]) continue;
+        long long blocks = (hi[q] - lo[q] + C::WPB - 1) / C::WPB;   // persistent grid
+        if (cap > 0 && blocks > cap) blocks = cap;
+        hipLaunchKernelGGL(ame_cov_mfma_kernel<R>, dim3((unsigned)blocks), dim3(256), 0, st, *dm, *a, lo[q],
+                           hi[q], q);
+        if (hipGetLastError() != hipSuccess) return -3;
+    }
+    return 0;
+}
+
 template <int R>
 static int launch_cov(const ame_dims* dm, const ame_cov_args* a, hipStream_t st) {
+    if constexpr (R >= AME_COV_MFMA_MIN_R) return launch_cov_mfma<R>(dm, a, st);
     using C = CovCfg<R>;
     const long long total = (long long)dm->T_local * dm->n;
     const long long waves = (total + C::MPW - 1) / C::MPW;
