@@ -251,6 +251,28 @@ ame_cov_kernel(ame_dims dm, ame_cov_args a) {
 #endif
 typedef double ame_d4 __attribute__((ext_vector_type(4)));
 
+#ifdef AME_COV_STAMPS
+// Diagnostic build only (tools/build_variant.py --defs=AME_COV_STAMPS): wave 0
+// of block 0 records s_memtime at the phase boundaries of its first 16
+// covariances (tools/cov_stamps.py).
+__device__ unsigned long long g_cov_st[16 * 8];
+#define CST(slot)                                                                              \
+    do {                                                                                       \
+        if (blockIdx.x == 0 && w == 0 && lane == 0 && it < 16) {                               \
+            unsigned long long t_;                                                             \
+            __builtin_amdgcn_sched_barrier(0);                                                 \
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");        \
+            __builtin_amdgcn_sched_barrier(0);                                                 \
+            g_cov_st[it * 8 + (slot)] = t_;                                                    \
+        }                                                                                      \
+    } while (0)
+extern "C" int ame_debug_read_cov_stamps(unsigned long long* st) {
+    return hipMemcpyFromSymbol(st, HIP_SYMBOL(g_cov_st), sizeof(g_cov_st), 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#else
+#define CST(slot) do { } while (0)
+#endif
+
 template <int R>
 struct CovM {
     static constexpr int B = 2 * R, D = B + 2, DD = D * D;
@@ -305,8 +327,11 @@ __device__ __forceinline__ double cov_mtrace(const ame_d4 (&tile)[CovM<R>::NTL],
 
 // Covariances [mc0, mc1) of the local block, all with the same trace matrix:
 // msel 0 = S0^-1 (slice 0), 1 = Q^-1 (the host splits the launch at slice 1)
+#ifndef AME_COV_MFMA_WAVES
+#define AME_COV_MFMA_WAVES 3
+#endif
 template <int R>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, AME_COV_MFMA_WAVES)
 ame_cov_mfma_kernel(ame_dims dm, ame_cov_args a, long long mc0, long long mc1, int msel) {
     using C = CovM<R>;
     constexpr int B = C::B, D = C::D, DD = C::DD, NT = C::NT, BP = C::BP, NTL = C::NTL, NWT = C::NWT,
@@ -323,7 +348,9 @@ ame_cov_mfma_kernel(ame_dims dm, ame_cov_args a, long long mc0, long long mc1, i
     const long long stride = (long long)gridDim.x * WPB;
     const int g = lane >> 4, c = lane & 15;
     double* pb = pbuf[w];
-    for (long long mc = mc0 + (long long)blockIdx.x * WPB + w; mc < mc1; mc += stride) {
+    int it = 0;   // (stamps only)
+    for (long long mc = mc0 + (long long)blockIdx.x * WPB + w; mc < mc1; mc += stride, ++it) {
+        CST(0);
         const float* A = a.cov + mc * DD;
         const double a00 = A[0], a01 = A[1], a10 = A[D], a11 = A[D + 1];
         float2 u[NT];   // A[2 + row][0..1], row = 16 I + c
@@ -366,6 +393,7 @@ ame_cov_mfma_kernel(ame_dims dm, ame_cov_args a, long long mc0, long long mc1, i
             for (int v = 0; v < 4; ++v) tm = fma(wq[(4 * t + v) * 64 + lane], (double)ft[t][v], tm);
             if (t & 1) asm volatile("" : "+v"(tm)::"memory");
         }
+        CST(1);
         // ---- Schur complement of the (a,b) block: S = A22 - U (A_aa^-1 U^T) ----
         const double det2 = a00 * a11 - a01 * a10;
         const double id2 = 1.0 / det2;
@@ -389,8 +417,8 @@ ame_cov_mfma_kernel(ame_dims dm, ame_cov_args a, long long mc0, long long mc1, i
                 }
         }
         // ---- blocked LDL^T, panels of 4 columns ----
-        double prod = det2;
-        int e2 = 0, neg = det2 < 0.0 ? 1 : 0;
+        double prod = det2;   // its sign is the determinant's (frexp keeps it)
+        int e2 = 0;
         bool zero = det2 == 0.0;
         // one tile column at a time (compile-time tile indices), its 4 panels in
         // a loop (a full unroll let the compiler hoist across panels: 376 VGPRs)
@@ -420,7 +448,6 @@ ame_cov_mfma_kernel(ame_dims dm, ame_cov_args a, long long mc0, long long mc1, i
                     const int P = 4 * p + kk;
                     const double piv = ame::lane_bcast(x[kk], P);
                     zero |= piv == 0.0;
-                    neg ^= piv < 0.0 ? 1 : 0;
                     prod *= piv;
                     if (kk == 3 && (sub & 1)) {   // every 8 pivots
                         int ex;
@@ -449,27 +476,34 @@ ame_cov_mfma_kernel(ame_dims dm, ame_cov_args a, long long mc0, long long mc1, i
                         xb[I] = pb[g * 64 + 16 * I + c];
                         xa[I] = -xb[I] * rk;
                     }
-#pragma unroll
-                    for (int I = Jp + 1; I < NT; ++I)
-#pragma unroll
-                        for (int J = Jp + 1; J <= I; ++J)
-                            tile[cov_ti(I, J)] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[I], xb[J], tile[cov_ti(I, J)], 0, 0, 0);
+                    // the next panel's tile column first: its extraction waits
+                    // only for those MFMAs
                     if (sub < 3) {
 #pragma unroll
                         for (int I = Jp; I < NT; ++I)
                             tile[cov_ti(I, Jp)] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[I], xb[Jp], tile[cov_ti(I, Jp)], 0, 0, 0);
                     }
+#pragma unroll
+                    for (int J = Jp + 1; J < NT; ++J)
+#pragma unroll
+                        for (int I = J; I < NT; ++I)
+                            tile[cov_ti(I, J)] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[I], xb[J], tile[cov_ti(I, J)], 0, 0, 0);
                 }
             }
         };
         static_assert(NT >= 1 && NT <= 4, "r <= 32");
+        CST(2);
         tile_column(std::integral_constant<int, 0>{});
+        CST(3);
         if constexpr (NT > 1) tile_column(std::integral_constant<int, 1>{});
+        CST(4);
         if constexpr (NT > 2) tile_column(std::integral_constant<int, 2>{});
+        CST(5);
         if constexpr (NT > 3) tile_column(std::integral_constant<int, 3>{});
+        CST(6);
         double ld = log(fabs(prod)) + (double)e2 * 0.69314718055994530942;
         if (zero) ld = -INFINITY;
-        else if (neg) ld = NAN;
+        else if (prod < 0.0) ld = NAN;
         tr = wave_sum(tr);
         tm = wave_sum(tm);
         if (lane == 0) {
@@ -479,6 +513,7 @@ ame_cov_mfma_kernel(ame_dims dm, ame_cov_args a, long long mc0, long long mc1, i
             o[2] = msel ? tm : 0.0;
             o[3] = msel ? 0.0 : tm;
         }
+        CST(7);
     }
 }
 
