@@ -534,6 +534,17 @@ __device__ __forceinline__ void v2_block_role(int TL, int& slice, int& role) {
     }
 }
 
+// Phase-3 block tiling (AME_PH3_BLOCK): edge PB = ceil(D / 22), so the lower
+// triangle of blocks (<= 22 * 23 / 2 = 253) fits the workgroup's 256 threads
+#ifndef AME_PH3_BLOCK
+#define AME_PH3_BLOCK 1
+#endif
+template <int D>
+struct Ph3 {
+    static constexpr int PB = (D + 21) / 22, NBK = (D + PB - 1) / PB, NBT = NBK * (NBK + 1) / 2;
+    static_assert(NBT <= AME_NT, "phase-3 blocks exceed the workgroup");
+};
+
 template <int R, int MODE>
 __global__ void __launch_bounds__(AME_NT)
 ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
@@ -746,6 +757,14 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         if (lk[qq] >= 0 && lk[qq] == lm[qq]) dflag |= 1u << qq;
         if (lk[qq] >= 0 && ((lk[qq] < 2) != (lm[qq] < 2))) oflag |= 1u << qq;
     }
+    // phase 3 in PB x PB blocks of the lower triangle, one block per thread:
+    // a block reads its PB rows of L and PB rows of R once (instead of one L
+    // row and one R row per entry: 64 of the 84 bytes an entry read from LDS)
+    // (kind 23 keeps the per-entry form: with the block form its worker code
+    // path spilled)
+    constexpr bool PH3B = AME_PH3_BLOCK && MODE != 3;
+    int pkb = -1, pmb = -1;
+    if (PH3B && tid < Ph3<D>::NBT) tri_decode(tid, pkb, pmb);
 
     // ---- helpers ----
     float2 ypf[AME_YPF];
@@ -1664,6 +1683,53 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             // Branch-free: every round but the last has an entry on every
             // thread (LTF full rounds); flags select the variant's value; a
             // diagonal entry stores its (equal) mirror value twice.
+            if constexpr (PH3B) {
+            if (pkb >= 0) {
+                constexpr int PB = Ph3<D>::PB;
+                const int k0 = PB * pkb, m0 = PB * pmb;
+                // every LDS read of the block first, then the arithmetic and stores
+                double ul[PB][4], ur[PB][4], kr[PB][PB];
+                float ckm[PB][PB], cmk[PB][PB], nd[PB];
+#pragma unroll
+                for (int q = 0; q < PB; ++q) {
+                    const int k = min(k0 + q, D - 1), m = min(m0 + q, D - 1);
+                    const double2 l01 = *(const double2*)(upd + 8 * k), l23 = *(const double2*)(upd + 8 * k + 2);
+                    const double2 r01 = *(const double2*)(upd + 8 * m + 4), r23 = *(const double2*)(upd + 8 * m + 6);
+                    ul[q][0] = l01.x; ul[q][1] = l01.y; ul[q][2] = l23.x; ul[q][3] = l23.y;
+                    ur[q][0] = r01.x; ur[q][1] = r01.y; ur[q][2] = r23.x; ur[q][3] = r23.y;
+                    nd[q] = ndiag[k];   // naive only
+                }
+#pragma unroll
+                for (int x = 0; x < PB; ++x)
+#pragma unroll
+                    for (int y = 0; y < PB; ++y) {
+                        const int k = min(k0 + x, D - 1), m = min(m0 + y, D - 1);
+                        kr[x][y] = K[k * KS + m];
+                        ckm[x][y] = cob[k * D + m];
+                        cmk[x][y] = cob[m * D + k];
+                    }
+#pragma unroll
+                for (int x = 0; x < PB; ++x)
+#pragma unroll
+                    for (int y = 0; y < PB; ++y) {
+                        const int k = k0 + x, m = m0 + y;
+                        if (k >= D || m >= D || (pkb == pmb && y > x)) continue;
+                        const double c = kr[x][y] - (ul[x][0] * ur[y][0] + ul[x][1] * ur[y][1]);
+                        const double kn = c + (ul[x][2] * ur[y][2] + ul[x][3] * ur[y][3]);
+                        const bool dg = k == m, ob = (k < 2) != (m < 2);
+                        float c32 = (float)c;
+                        c32 = (is_bad && ob) ? 0.f : c32;
+                        c32 = dg ? c32 + 1e-6f : c32;
+                        c32 = is_naive ? (dg ? nd[x] : 0.f) : c32;
+                        const float vkm = mul_add_rn(lr, c32, om, ckm[x][y]);
+                        const float vmk = mul_add_rn(lr, c32, om, cmk[x][y]);
+                        K[k * KS + m] = kn;
+                        K[m * KS + k] = kn;
+                        cst[k * D + m] = vkm;
+                        cst[m * D + k] = vmk;
+                    }
+            }
+            } else {
             constexpr int QB = 5;   // 9 entries per thread at d = 66: rounds of 5 and 4
             constexpr int LTF = NLT / AME_NT;
             // opaque per step: hoisted out of the loop, each flag test became a
@@ -1707,6 +1773,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                     cst[k * D + m] = vkm;
                     cst[m * D + k] = vmk;
                 }
+            }
             }
             }
             STAMPW(14, 0);
