@@ -30,6 +30,9 @@
 //    config 3; two columns: 0.21 ms, profiles/r03_cov_ab.txt.)
 // The input is taken as symmetric: the sweep writes symmetric covariances and
 // the reference's initialisation symmetrises (structured_mf.py:94-96).
+// Two forms: the column-per-lane LDL^T below (r < AME_COV_MFMA_MIN_R) and, for
+// wide states, a blocked LDL^T on fp64 MFMA (ame_cov_mfma_kernel, further down;
+// DESIGN.md §4 K2, profiles/r05_cov_ab.txt).
 #include "ame_common.h"
 #include "ame_wave.h"
 #include <type_traits>
