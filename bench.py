@@ -443,6 +443,9 @@ def main():
     ap.add_argument("--sweep-kernel", type=int, default=0,
                     help="sweep kernel request (include/ame_amd.h enum ame_sweep_kind_code; "
                          "0 = AUTO, the production choice)")
+    ap.add_argument("--elbo-cus", type=int, default=0,
+                    help="run the ELBO kernels on a CU-masked stream over this many CUs beside "
+                         "the sweep (engine option elbo_cus; needs --sweep-kernel 22 or 24)")
     ap.add_argument("--config5-full", action="store_true",
                     help="BASELINE config 5's own workload (n=4096, T=256, r=32) three-way on "
                          "this one GPU; prints its own JSON line instead of the metric")
@@ -461,6 +464,8 @@ def main():
     use_dist = world > 1 or args.force_dist
     if args.config5_full:
         c5opts = {"sweep_kernel": args.sweep_kernel} if args.sweep_kernel else None
+        if args.elbo_cus:
+            c5opts = dict(c5opts or {}, elbo_cus=args.elbo_cus)
         if args.no_pipeline:
             c5opts = dict(c5opts or {}, pipeline=False)
         out = config5_full(dev, steps=args.steps if args.steps != 50 else 3,
@@ -480,6 +485,8 @@ def main():
     opts = {"pipeline": False} if args.no_pipeline else {}
     if args.sweep_kernel:
         opts["sweep_kernel"] = args.sweep_kernel
+    if args.elbo_cus:
+        opts["elbo_cus"] = args.elbo_cus
     opts = opts or None
     if args.variant == "naive":
         vi = TemporalAMENaiveMFVI(model, learning_rate=args.lr, device=dev,
@@ -593,6 +600,7 @@ def main():
                 "n_nodes": n, "n_time_total": T_total, "latent_dim": r, "d": d,
                 "variant": args.variant, "parallelism": f"time-sharded x{world}",
                 "sweep_kind": int(vi.engine.sweep_kind),
+                **({"elbo_cus": args.elbo_cus} if args.elbo_cus else {}),
             },
             "roofline": {"bound": "hbm", "kernel": "sweep", "achieved": sw["achieved_GBs"],
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": sw["frac"],

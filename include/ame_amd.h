@@ -75,6 +75,11 @@ enum ame_variant { AME_GOOD = 0, AME_BAD = 1, AME_NAIVE = 2 };
  *                         slices fit at once and the kernel orders itself slice
  *                         by slice (done flags, wait_epoch), so sweeps and slice
  *                         groups pipeline like AME_SWEEP_V3; d > 64, n <= 4096
+ *   AME_SWEEP_V2_W6       v2 plus six GEMV worker workgroups per slice (7 per
+ *                         slice), not pipelined: BASELINE config 5's 32 slices
+ *                         hold 224 CUs, so the ELBO kernels can run beside the
+ *                         next sweep on the other 32 (CU-masked streams,
+ *                         ame_stream_create_cu_range); n <= 4224
  * Requests (resolved by ame_sweep_kind for given dims):
  *   AME_SWEEP_AUTO        V3 when the shape fits it, else AME_SWEEP_V2_AUTO
  *   AME_SWEEP_V2_AUTO     V2_WORKERS when their workgroups are co-resident, else
@@ -89,7 +94,8 @@ enum ame_sweep_kind_code {
     AME_SWEEP_V2_LDS = 20,
     AME_SWEEP_V2_HBM = 21,
     AME_SWEEP_V2_WORKERS = 22,
-    AME_SWEEP_V2_PIPE = 23
+    AME_SWEEP_V2_PIPE = 23,
+    AME_SWEEP_V2_W6 = 24
 };
 
 /* ame_sweep_args.flags */
@@ -233,6 +239,15 @@ long long ame_elbo_work_size(const ame_dims* dims);
  * (its per-workgroup partials land in args->work; args->out is NOT written).
  * Not part of an iteration; bench.py times the pair kernel alone with it. */
 int ame_elbo_pairs_diag(const ame_dims* dims, const ame_elbo_args* args, void* stream);
+
+/* A HIP stream whose kernels run only on compute units [first_cu, first_cu +
+ * num_cus) of the current device (hipExtStreamCreateWithCUMask); *stream
+ * receives the hipStream_t.  With AME_SWEEP_V2_W6 the engine puts the sweep on
+ * one CU range and the ELBO kernels on the rest, so they run side by side
+ * instead of queueing behind the sweep's workgroups.  Replaces nothing in the
+ * reference (CPU).  ame_stream_destroy releases it. */
+int ame_stream_create_cu_range(int first_cu, int num_cus, void** stream);
+int ame_stream_destroy(void* stream);
 
 /* Pin + map host memory for device access; *dev receives the device address
  * (utility; the multi-GPU path uses the peer buffers below). */

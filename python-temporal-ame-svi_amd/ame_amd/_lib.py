@@ -20,7 +20,7 @@ AME_STATUS_STALE_EPOCH = 8
 AME_PEER_HANDLE_BYTES = 64
 # sweep kernel requests / kinds (enum ame_sweep_kind_code)
 AME_SWEEP_AUTO, AME_SWEEP_V2_SINGLE, AME_SWEEP_V2_AUTO, AME_SWEEP_V3 = 0, 1, 2, 3
-AME_SWEEP_V2_LDS, AME_SWEEP_V2_HBM, AME_SWEEP_V2_WORKERS, AME_SWEEP_V2_PIPE = 20, 21, 22, 23
+AME_SWEEP_V2_LDS, AME_SWEEP_V2_HBM, AME_SWEEP_V2_WORKERS, AME_SWEEP_V2_PIPE, AME_SWEEP_V2_W6 = 20, 21, 22, 23, 24
 AME_SWEEP_FLAG_NEXT_GROUP = 1
 # ELBO pair kernels (enum ame_pairs_kernel_code)
 AME_PAIRS_AUTO, AME_PAIRS_V1, AME_PAIRS_V2 = 0, 1, 2
@@ -58,6 +58,7 @@ class ame_elbo_args(ctypes.Structure):
 # every symbol include/ame_amd.h declares (checked by tests/test_capi.py)
 EXPORTS = ("ame_pack_y", "ame_pack_y_size", "ame_sweep", "ame_sweep_kind", "ame_sweep_work_size", "ame_sweep_orders_slices", "ame_sweep_max_slices", "ame_sweep_lds_bytes", "ame_cov",
            "ame_elbo", "ame_elbo_work_size", "ame_elbo_pairs_diag", "ame_host_register", "ame_host_unregister",
+           "ame_stream_create_cu_range", "ame_stream_destroy",
            "ame_peer_alloc", "ame_peer_free", "ame_peer_open", "ame_peer_close",
            "ame_peer_probe", "ame_peer_read_u64", "ame_peer_clear",
            "ame_supported_r", "ame_last_error", "ame_version", "ame_align_work_size",
@@ -93,6 +94,8 @@ def _declare(L):
     L.ame_sweep_work_size.argtypes = [P(ame_dims), ctypes.c_int]
     L.ame_sweep_work_size.restype = ctypes.c_longlong
     L.ame_supported_r.argtypes = [P(ctypes.c_int), ctypes.c_int]
+    L.ame_stream_create_cu_range.argtypes = [ctypes.c_int, ctypes.c_int, P(c_vp)]
+    L.ame_stream_destroy.argtypes = [c_vp]
     L.ame_host_register.argtypes = [c_vp, ctypes.c_ulonglong, P(c_vp)]
     L.ame_host_unregister.argtypes = [c_vp]
     L.ame_peer_alloc.argtypes = [ctypes.c_ulonglong, P(c_vp), c_vp]

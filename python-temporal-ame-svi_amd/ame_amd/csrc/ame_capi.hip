@@ -8,7 +8,7 @@
 
 int ame_sweep_dispatch(const ame_dims*, const ame_sweep_args*, hipStream_t);
 int ame_sweep_blocks_per_cu(int n, int r, int mode);
-int ame_sweep_workers_fit(const ame_dims* dm, int mode);   // mode 2: kind 22, 3: kind 23
+int ame_sweep_workers_fit(const ame_dims* dm, int mode);   // mode 2: kind 22, 3: kind 23, 4: kind 24
 int ame_sweep3_dispatch(const ame_dims*, const ame_sweep_args*, hipStream_t);
 int ame_sweep3_supported(int n, int r);
 int ame_sweep3_blocks_per_cu(int n, int r);
@@ -83,6 +83,32 @@ int ame_supported_r(int* out, int cap) {
     AME_FOR_EACH_R(X)
 #undef X
     return c;
+}
+
+#define AME_MAX_CUS 1024
+static int device_cus();
+int ame_stream_create_cu_range(int first_cu, int num_cus, void** stream) {
+    if (!stream) return fail("ame_stream_create_cu_range: NULL");
+    const int cus = device_cus();
+    if (first_cu < 0 || num_cus < 1 || first_cu + num_cus > cus)
+        return fail("ame_stream_create_cu_range: CUs [%d, %d) outside the device", first_cu,
+                    first_cu + num_cus);
+    uint32_t mask[(AME_MAX_CUS + 31) / 32] = {0};
+    if (cus > AME_MAX_CUS) return fail("ame_stream_create_cu_range: %d CUs", cus);
+    for (int c = first_cu; c < first_cu + num_cus; ++c) mask[c / 32] |= 1u << (c % 32);
+    hipStream_t s = nullptr;
+    const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)((cus + 31) / 32), mask);
+    if (e != hipSuccess) {
+        snprintf(g_err, sizeof(g_err), "ame_stream_create_cu_range: %s", hipGetErrorString(e));
+        return -1;
+    }
+    *stream = (void*)s;
+    return 0;
+}
+
+int ame_stream_destroy(void* stream) {
+    if (!stream) return fail("ame_stream_destroy: NULL");
+    return hipStreamDestroy((hipStream_t)stream) == hipSuccess ? 0 : fail("ame_stream_destroy failed");
 }
 
 int ame_host_register(void* host, unsigned long long bytes, void** dev) {
@@ -193,7 +219,7 @@ static bool v2_block_in_lds(int n, int r) { return !sweep_lds_layout(n, r, 0).m_
 static bool v2_single_fits(int n, int r) { return sweep_lds_layout(n, r, 1).total <= AME_LDS_MAX; }
 static bool is_concrete(int k) {
     return k == AME_SWEEP_V3 || k == AME_SWEEP_V2_LDS || k == AME_SWEEP_V2_HBM || k == AME_SWEEP_V2_WORKERS ||
-           k == AME_SWEEP_V2_PIPE;
+           k == AME_SWEEP_V2_PIPE || k == AME_SWEEP_V2_W6;
 }
 
 // Request -> concrete kernel for these dims (-1 + message when it cannot run).
@@ -228,6 +254,9 @@ static int resolve_kind(const ame_dims* d, int request) {
             if (ame_sweep_workers_fit(d, 3)) return AME_SWEEP_V2_PIPE;
             return fail("ame_sweep: the pipelined GEMV-worker sweep does not fit n=%d, T_local=%d",
                         n, d->T_local);
+        case AME_SWEEP_V2_W6:
+            if (ame_sweep_workers_fit(d, 4)) return AME_SWEEP_V2_W6;
+            return fail("ame_sweep: the six-worker sweep does not fit n=%d, T_local=%d", n, d->T_local);
         default:
             return fail("ame_sweep: unknown sweep kind request %d", request);
     }
@@ -241,6 +270,7 @@ long long ame_sweep_lds_bytes(int n, int r, int kind) {
         case AME_SWEEP_V2_HBM: return ame_v2_mode_lds(n, r, 1);
         case AME_SWEEP_V2_WORKERS: return ame_v2_mode_lds(n, r, 2);
         case AME_SWEEP_V2_PIPE: return ame_v2_mode_lds(n, r, 3);
+        case AME_SWEEP_V2_W6: return ame_v2_mode_lds(n, r, 4);
         default: return 0;
     }
 }
@@ -268,6 +298,11 @@ int ame_sweep_max_slices(int n, int r, int request) {
             ame_dims one = {n, r, 1, 0, 1, 0};
             if (!ame_sweep_workers_fit(&one, 3)) return 0;
             return ame_sweep_blocks_per_cu(n, r, 3) * cus / (1 + AME_GW_P);
+        }
+        case AME_SWEEP_V2_W6: {
+            ame_dims one = {n, r, 1, 0, 1, 0};
+            if (!ame_sweep_workers_fit(&one, 4)) return 0;
+            return ame_sweep_blocks_per_cu(n, r, 4) * cus / (1 + AME_GW_6);
         }
         default:
             return 0;
@@ -299,6 +334,7 @@ long long ame_sweep_work_size(const ame_dims* dims, int kind) {
         // partial ring, then the precomputed right AR terms
         case AME_SWEEP_V2_WORKERS: return ame_v2_ring_doubles(dims, 2) + ame_v2_arr_doubles(dims);
         case AME_SWEEP_V2_PIPE: return ame_v2_ring_doubles(dims, 3) + ame_v2_arr_doubles(dims);
+        case AME_SWEEP_V2_W6: return ame_v2_ring_doubles(dims, 4) + ame_v2_arr_doubles(dims);
         default: return fail("ame_sweep_work_size: %d is not a concrete sweep kind", kind);
     }
 }
@@ -333,7 +369,7 @@ int ame_sweep(const ame_dims* dims, const ame_sweep_args* a, void* stream) {
         return fail("ame_sweep: the work buffer holds %d doubles, kind %d needs more", (int)a->work_doubles, kind);
     if (a->wait_epoch != 0 && (!ame_sweep_orders_slices(dims->n, dims->r, kind) || !a->done))
         return fail("ame_sweep: wait_epoch needs a kernel that orders slices (kind %d) and a done array", kind);
-    const int maxs = (kind == AME_SWEEP_V2_WORKERS || kind == AME_SWEEP_V2_PIPE)
+    const int maxs = (kind == AME_SWEEP_V2_WORKERS || kind == AME_SWEEP_V2_PIPE || kind == AME_SWEEP_V2_W6)
                           ? dims->T_local   // resolve_kind checked that the launch co-resides
                           : ame_sweep_max_slices(dims->n, dims->r, kind);
     if (dims->T_local > maxs)

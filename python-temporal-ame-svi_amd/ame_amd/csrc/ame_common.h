@@ -143,8 +143,22 @@ __host__ __device__ inline SweepLds sweep_lds_layout(int n, int R, int force_glo
 #ifndef AME_GW_P_NREG
 #define AME_GW_P_NREG 152
 #endif
-__host__ __device__ inline int ame_v2_nworkers(int mode) { return mode == 3 ? AME_GW_P : AME_GW; }
-__host__ __device__ inline int ame_v2_maxpw(int mode) { return mode == 3 ? AME_GW_P_MAXPW : AME_GW_MAXPW; }
+// six-worker v2 sweep (kind AME_SWEEP_V2_W6, MODE 4): 7 workgroups per slice, so
+// config 5's 32 slices hold 224 CUs and leave 32 to the ELBO kernels on a
+// CU-masked stream (engine option elbo_cus); a worker wave holds up to 176
+// nodes (n <= 6 * 4 * 176): kind 22's 152 in registers, 24 in LDS
+#define AME_GW_6 6
+#define AME_GW_6_MAXPW 176
+#define AME_GW_6_NREG 152
+__host__ __device__ constexpr int ame_v2_nworkers(int mode) {
+    return mode == 3 ? AME_GW_P : (mode == 4 ? AME_GW_6 : AME_GW);
+}
+__host__ __device__ constexpr int ame_v2_maxpw(int mode) {
+    return mode == 3 ? AME_GW_P_MAXPW : (mode == 4 ? AME_GW_6_MAXPW : AME_GW_MAXPW);
+}
+__host__ __device__ constexpr int ame_v2_nreg(int mode) {
+    return mode == 3 ? AME_GW_P_NREG : (mode == 4 ? AME_GW_6_NREG : AME_GW_MAXPW);
+}
 
 // Tag of worker partial m of sweep `epoch` in the partial ring.  Bit 31 is
 // always set, so a slot the launch zeroed can never match (an all-zero word
@@ -159,8 +173,8 @@ __host__ __device__ inline uint32_t ame_gw_tag(uint32_t epoch, int m) {
 __host__ __device__ inline long long ame_v2_worker_lds(int n, int R, int mode = 2) {
     const int nw = ame_v2_nworkers(mode);
     const int NW = (n + nw - 1) / nw, ZN = 4 * ame_v2_maxpw(mode);
-    // zb, red, and (MODE 3) the LDS-held node slots [4 waves][MAXPW - NREG][64]
-    const long long mld = mode == 3 ? 4LL * 4 * (AME_GW_P_MAXPW - AME_GW_P_NREG) * 64 : 0;
+    // zb, red, and (MODES 3, 4) the LDS-held node slots [4 waves][MAXPW - NREG][64]
+    const long long mld = 4LL * 4 * (ame_v2_maxpw(mode) - ame_v2_nreg(mode)) * 64;
     return ame_align16(8LL * (NW > ZN ? NW : ZN)) + ame_align16(4LL * 4 * (2 * R + 2)) + mld;
 }
 __host__ __device__ inline long long ame_v2_mode_lds(int n, int R, int mode) {

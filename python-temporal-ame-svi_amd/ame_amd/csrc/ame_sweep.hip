@@ -279,8 +279,8 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
                                             const int t, const int g) {
     constexpr int D = 2 + 2 * R, M2 = 2 * R, PW = M2 + 2;
     // MODE 2: seven workers per slice (kind 22); MODE 3: four (kind 23, pipelined)
-    constexpr int NG = (MODE == 3) ? AME_GW_P : AME_GW;
-    constexpr int MAXPW = (MODE == 3) ? AME_GW_P_MAXPW : AME_GW_MAXPW;
+    constexpr int NG = ame_v2_nworkers(MODE);
+    constexpr int MAXPW = ame_v2_maxpw(MODE);
     const int n = dm.n, TL = dm.T_local;
     const int NW = (n + NG - 1) / NG, base = g * NW;
     const int cnt = max(0, min(n, base + NW) - base);
@@ -354,7 +354,7 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
     // MODE 3 may hold more slots per wave than registers allow: the first NREG in
     // registers, the rest
     // in this workgroup's LDS past zb / red ([wave][slot][lane], conflict-free)
-    constexpr int NREG = (MODE == 3) ? AME_GW_P_NREG : MAXPW, NLD = MAXPW - NREG;
+    constexpr int NREG = ame_v2_nreg(MODE), NLD = MAXPW - NREG;
     float* mld = (float*)(smem + ame_align16(8LL * (NW > ZN ? NW : ZN)) + ame_align16(4LL * 4 * PW));
     float mreg[NREG];
 #pragma unroll
@@ -518,7 +518,7 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
 // partials stay in that XCD's L2.
 template <int MODE>
 __device__ __forceinline__ void v2_block_role(int TL, int& slice, int& role) {
-    constexpr int NG = (MODE == 3) ? AME_GW_P : AME_GW;
+    constexpr int NG = ame_v2_nworkers(MODE);
     const int b = blockIdx.x;
     if (MODE == 3 && (TL & 7) == 0) {
         const int per = TL >> 3, w = b >> 3;
@@ -550,7 +550,7 @@ __global__ void __launch_bounds__(AME_NT)
 ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     // MODE 2: seven GEMV workers per slice (kind 22); MODE 3: four, pipelined (kind 23)
     constexpr bool MG = MODE == 1, WK = MODE >= 2, PIPE = MODE == 3;
-    constexpr int NGW = PIPE ? AME_GW_P : AME_GW;
+    constexpr int NGW = ame_v2_nworkers(MODE);
     constexpr int D = 2 + 2 * R, M2 = 2 * R, KS = D + 1, US = (M2 + 15) / 16;
     constexpr int KH = (D + 63) / 64;   // state rows per solver lane
     constexpr int VEC = (R % 4 == 0) ? 4 : ((R % 2 == 0) ? 2 : 1);
@@ -760,9 +760,9 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     // phase 3 in PB x PB blocks of the lower triangle, one block per thread:
     // a block reads its PB rows of L and PB rows of R once (instead of one L
     // row and one R row per entry: 64 of the 84 bytes an entry read from LDS)
-    // (kind 23 keeps the per-entry form: with the block form its worker code
-    // path spilled)
-    constexpr bool PH3B = AME_PH3_BLOCK && MODE != 3;
+    // (kinds 23 and 24 keep the per-entry form: with the block form their
+    // LDS-slot worker code path spilled)
+    constexpr bool PH3B = AME_PH3_BLOCK && MODE != 3 && MODE != 4;
     int pkb = -1, pmb = -1;
     if (PH3B && tid < Ph3<D>::NBT) tri_decode(tid, pkb, pmb);
 
@@ -1882,6 +1882,7 @@ static int launch_sweep(const ame_dims* dm, const ame_sweep_args* a, hipStream_t
     switch (a->kind) {
         case AME_SWEEP_V2_WORKERS: return launch_sweep_t<R, 2>(dm, a, st);
         case AME_SWEEP_V2_PIPE: return launch_sweep_t<R, 3>(dm, a, st);
+        case AME_SWEEP_V2_W6: return launch_sweep_t<R, 4>(dm, a, st);
         case AME_SWEEP_V2_HBM: return launch_sweep_t<R, 1>(dm, a, st);
         case AME_SWEEP_V2_LDS: return launch_sweep_t<R, 0>(dm, a, st);
         default: return -1;
@@ -1895,6 +1896,7 @@ static int sweep_occupancy(int n, int mode) {
         case 1: return sweep_occupancy_t<R, 1>(n);
         case 2: return sweep_occupancy_t<R, 2>(n);
         case 3: return sweep_occupancy_t<R, 3>(n);
+        case 4: return sweep_occupancy_t<R, 4>(n);
         default: return 0;
     }
 }
@@ -1924,8 +1926,9 @@ int AME_PFN(ame_sweep_blocks_per_cu)(int n, int r, int mode) {
 int AME_PFN(ame_sweep_workers_fit)(const ame_dims* dm, int mode) {
     switch (dm->r) {
 #define X(RR) \
-    case RR: return (mode == 3 ? workers_fit<RR, 3>(dm->n, dm->T_local) \
-                               : workers_fit<RR, 2>(dm->n, dm->T_local)) ? 1 : 0;
+    case RR: return (mode == 3   ? workers_fit<RR, 3>(dm->n, dm->T_local) \
+                     : mode == 4 ? workers_fit<RR, 4>(dm->n, dm->T_local) \
+                                 : workers_fit<RR, 2>(dm->n, dm->T_local)) ? 1 : 0;
         AME_FOR_EACH_R(X)
 #undef X
         default: return 0;

@@ -59,6 +59,10 @@ class Shard:
     world: int = 1
 
 
+# CU-masked streams (EngineOptions.elbo_cus), per (device, first CU, CUs, slot)
+_CU_STREAMS = {}
+
+
 @dataclass
 class EngineOptions:
     """Execution choices of one engine.  Nothing is read from the environment:
@@ -76,6 +80,13 @@ class EngineOptions:
                   (:func:`derive_spec_depth`)
     slice_group   at most this many local slices per launch (0: as many as fit)
     pairs_kernel  ELBO pair kernel (``_lib.AME_PAIRS_*``; 0 = default)
+    elbo_cus      > 0: run the ELBO kernels on their own CU-masked stream over
+                  compute units [0, elbo_cus) and the sweep streams over the
+                  rest (ame_stream_create_cu_range), so iteration k's ELBO runs
+                  beside sweep k+1 instead of queueing behind its workgroups.
+                  Needs a non-pipelined GEMV-worker kind (sweep_kernel 22 or 24)
+                  whose launch fits the remaining CUs (kind 24 at config 5's
+                  rank shape: 32 slices x 7 workgroups = 224 CUs, elbo_cus 32)
     """
     sweep_kernel: int = 0
     pipeline: bool = True
@@ -83,6 +94,7 @@ class EngineOptions:
     spec_depth: Optional[int] = None
     slice_group: int = 0
     pairs_kernel: int = 0
+    elbo_cus: int = 0
 
     @classmethod
     def coerce(cls, opts) -> "EngineOptions":
@@ -289,6 +301,18 @@ class DeviceEngine:
         if self.max_slices < 1:
             raise RuntimeError(f"ame_amd: no sweep kernel fits n={self.n}, r={self.r} "
                                f"(request {opt.sweep_kernel})")
+        self._cu_split = None
+        if opt.elbo_cus:
+            # ELBO beside the sweep: the sweep's launch must fit the CUs left to it
+            per_slice = {_lib.AME_SWEEP_V2_WORKERS: 8, _lib.AME_SWEEP_V2_W6: 7}.get(opt.sweep_kernel)
+            cus = int(torch.cuda.get_device_properties(self.dev).multi_processor_count)
+            if per_slice is None or not 0 < int(opt.elbo_cus) < cus:
+                raise ValueError("elbo_cus needs sweep_kernel 22 or 24 and 0 < elbo_cus < "
+                                 f"{cus} CUs (got {opt.elbo_cus}, kernel {opt.sweep_kernel})")
+            self.max_slices = min(self.max_slices, (cus - int(opt.elbo_cus)) // per_slice)
+            if self.max_slices < 1:
+                raise ValueError(f"elbo_cus={opt.elbo_cus} leaves no room for a slice")
+            self._cu_split = (int(opt.elbo_cus), cus)
         req = opt.sweep_kernel
         if req in (_lib.AME_SWEEP_AUTO, _lib.AME_SWEEP_V2_AUTO) and (
                 req == _lib.AME_SWEEP_V2_AUTO
@@ -344,7 +368,13 @@ class DeviceEngine:
         self._specs = collections.deque()   # (done events, ring slot) of sweeps started ahead
         # consecutive sweeps (or, pipelined, consecutive launches) alternate
         # between two high-priority streams
-        self.sweep_streams = [torch.cuda.Stream(device=self.dev, priority=-1) for _ in range(2)]
+        self.elbo_stream = None
+        if self._cu_split is None:
+            self.sweep_streams = [torch.cuda.Stream(device=self.dev, priority=-1) for _ in range(2)]
+        else:
+            ec, cus = self._cu_split
+            self.elbo_stream = self._cu_stream(0, ec)
+            self.sweep_streams = [self._cu_stream(ec, cus - ec, slot) for slot in range(2)]
         self._launch_ctr = 0
         self.done = torch.zeros(max(sh.T_local, 1), dtype=torch.int32, device=self.dev)
         kinds = set(self.group_kinds.values())
@@ -386,6 +416,37 @@ class DeviceEngine:
         # epoch-window check catching the resulting stale flags
         self._order_after_host_writes = True
         self._mark_host_writes()
+
+    def _cu_stream(self, first, num, slot=0):
+        """A stream over compute units [first, first + num) (C-ABI, HIP CU mask),
+        shared by every engine of the process and never destroyed: the caching
+        allocator keeps events on the streams its blocks were used on
+        (record_stream), so a stream must outlive every tensor an engine drops."""
+        key = (self.dev.index, int(first), int(num), int(slot))
+        st = _CU_STREAMS.get(key)
+        if st is None:
+            p = ctypes.c_void_p()
+            with torch.cuda.device(self.dev):
+                _lib.check(self.L.ame_stream_create_cu_range(int(first), int(num), ctypes.byref(p)),
+                           "ame_stream_create_cu_range")
+            st = _CU_STREAMS[key] = torch.cuda.ExternalStream(p.value, device=self.dev)
+        return st
+
+    def _elbo_stream_begin(self):
+        """The stream the ELBO kernels run on: the main stream, or (elbo_cus) the
+        CU-masked ELBO stream ordered after everything queued on the main one."""
+        if self.elbo_stream is None:
+            return self.stream
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        self.elbo_stream.wait_event(ev)
+        return self.elbo_stream
+
+    def _elbo_stream_end(self, st):
+        if st is not self.stream:   # later main-stream work (reading out) waits for it
+            ev = torch.cuda.Event()
+            ev.record(st)
+            self.stream.wait_event(ev)
 
     def _mark_host_writes(self):
         """Record the main-stream position after host-issued writes to the state
@@ -589,9 +650,12 @@ class DeviceEngine:
         """Covariance ELBO terms of the current covariances (no update)."""
         c = _lib.ame_cov_args(cov=_ptr(self.cov), consts=_ptr(self.consts),
                               cov_terms=_ptr(self.cov_terms))
-        tok = self._tic("cov")
-        _lib.check(self.L.ame_cov(ctypes.byref(self.dims), ctypes.byref(c), self._sp()), "ame_cov")
+        st = self._elbo_stream_begin()
+        tok = self._tic("cov", st)
+        _lib.check(self.L.ame_cov(ctypes.byref(self.dims), ctypes.byref(c),
+                                  ctypes.c_void_p(st.cuda_stream)), "ame_cov")
         self._toc(tok)
+        self._elbo_stream_end(st)
         self._cov_terms_valid = True
 
     def launch_elbo(self, pairs_only=False):
@@ -608,16 +672,19 @@ class DeviceEngine:
             cov_terms=_ptr(self.cov_terms), consts=_ptr(self.consts), phi=_ptr(self.phi),
             rinv=self.C.rinv4(), swap_consistent=1 if self.swap_consistent else 0,
             work=_ptr(self.work), out=_ptr(self.out), pairs_kernel=self.options.pairs_kernel)
+        st = self._elbo_stream_begin()
+        sp = ctypes.c_void_p(st.cuda_stream)
         if pairs_only:
-            tok = self._tic("pairs")
-            _lib.check(self.L.ame_elbo_pairs_diag(ctypes.byref(self.dims), ctypes.byref(e),
-                                                  self._sp()), "ame_elbo_pairs_diag")
+            tok = self._tic("pairs", st)
+            _lib.check(self.L.ame_elbo_pairs_diag(ctypes.byref(self.dims), ctypes.byref(e), sp),
+                       "ame_elbo_pairs_diag")
             self._toc(tok)
+            self._elbo_stream_end(st)
             return
-        tok = self._tic("elbo")
-        _lib.check(self.L.ame_elbo(ctypes.byref(self.dims), ctypes.byref(e), self._sp()),
-                   "ame_elbo")
+        tok = self._tic("elbo", st)
+        _lib.check(self.L.ame_elbo(ctypes.byref(self.dims), ctypes.byref(e), sp), "ame_elbo")
         self._toc(tok)
+        self._elbo_stream_end(st)
 
     def sums(self, speculate=0):
         """The 8 fp64 sums for the current state (all ranks reduced).  With
