@@ -49,15 +49,22 @@
 #define AME_STAMP_I0 256
 #define AME_STAMP_NPH 32
 __device__ unsigned long long g_ame_stamps[16 * AME_STAMP_NPH];
+// s_memrealtime (constant 100 MHz, one clock for the whole device) beside each
+// s_memtime stamp: the slice workgroup and its workers run on different CUs,
+// often different XCDs, whose s_memtime counters are not comparable
+__device__ unsigned long long g_ame_rt[16 * AME_STAMP_NPH];
+__device__ unsigned long long g_ame_wrt[16 * 8];
 #define STAMP(ph) STAMPW(ph, 0)
 #define STAMPW(ph, who)                                                                    \
     do {                                                                                   \
         if (stamp_on && tid == (who)) {                                                    \
-            unsigned long long t_;                                                         \
+            unsigned long long t_, r_;                                                     \
             __builtin_amdgcn_sched_barrier(0);                                             \
             asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");     \
+            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r_)::"memory"); \
             __builtin_amdgcn_sched_barrier(0);                                             \
             g_ame_stamps[(i - AME_STAMP_I0) * AME_STAMP_NPH + (ph)] = t_;                  \
+            g_ame_rt[(i - AME_STAMP_I0) * AME_STAMP_NPH + (ph)] = r_;                      \
         }                                                                                  \
     } while (0)
 // GEMV worker 0 of the middle slice: per node m in [I0+4, I0+20): loop top,
@@ -66,11 +73,13 @@ __device__ unsigned long long g_ame_wstamps[16 * 8];
 #define WSTAMP(ph)                                                                         \
     do {                                                                                   \
         if (t == TL / 2 && g == 0 && tid == 0 && m >= AME_STAMP_I0 + 4 && m < AME_STAMP_I0 + 20) { \
-            unsigned long long t_;                                                         \
+            unsigned long long t_, r_;                                                     \
             __builtin_amdgcn_sched_barrier(0);                                             \
             asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");     \
+            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r_)::"memory"); \
             __builtin_amdgcn_sched_barrier(0);                                             \
             g_ame_wstamps[(m - AME_STAMP_I0 - 4) * 8 + (ph)] = t_;                         \
+            g_ame_wrt[(m - AME_STAMP_I0 - 4) * 8 + (ph)] = r_;                             \
         }                                                                                  \
     } while (0)
 // phase-2 detail of the middle slice's waves 1-3 (WK): slot = 2 * wave-1 + {0: signalled, 1: reduce+AR done}
@@ -87,6 +96,13 @@ __device__ unsigned long long g_ame_p2stamps[16 * 16];
     } while (0)
 extern "C" int ame_debug_read_p2stamps(unsigned long long* host) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ame_p2stamps), sizeof(g_ame_p2stamps), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+extern "C" int ame_debug_read_rt(unsigned long long* main_rt, unsigned long long* worker_rt) {
+    if (hipMemcpyFromSymbol(main_rt, HIP_SYMBOL(g_ame_rt), sizeof(g_ame_rt), 0, hipMemcpyDeviceToHost) !=
+        hipSuccess)
+        return -1;
+    return hipMemcpyFromSymbol(worker_rt, HIP_SYMBOL(g_ame_wrt), sizeof(g_ame_wrt), 0,
                                hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 extern "C" int ame_debug_read_wstamps(unsigned long long* host) {

@@ -74,7 +74,8 @@ def run():
         vi = TemporalAMEStructuredMFVI(m, factorization=variant, learning_rate=0.01, device=dev,
                                        engine_options=opts)
     assert vi.engine.sweep_kind in (_lib.AME_SWEEP_V2_LDS, _lib.AME_SWEEP_V2_HBM,
-                                    _lib.AME_SWEEP_V2_WORKERS, _lib.AME_SWEEP_V2_PIPE), vi.engine.sweep_kind
+                                    _lib.AME_SWEEP_V2_WORKERS, _lib.AME_SWEEP_V2_PIPE,
+                                    _lib.AME_SWEEP_V2_W6), vi.engine.sweep_kind
     # one launch per sweep (the stamp buffers are per kernel, not per group)
     assert len(vi.engine.groups) == 1, vi.engine.groups
     vi.fit(max_iter=2, tolerance=0.0, verbose=False)
@@ -137,9 +138,27 @@ def run():
                 d = sorted(w[k][p] - w[k][p - 1] for k in range(16))[8]
                 print(f"    {nm:16s} +{d:7d}")
             # when partial m (worker) was stored vs main's step m-1 start (node m-1 = I0+3+k)
-            lead = [rows[k + 3][0] - w[k][4] for k in range(13) if rows[k + 3][0]]
-            print("    main step m-1 start minus partial m stored (cycles, >0: ready early):",
-                  sorted(lead)[len(lead) // 2] if lead else None)
+            # (s_memtime counters of different XCDs are not comparable: the lead
+            # uses the device-wide s_memrealtime recorded beside each stamp, 100 MHz)
+            if hasattr(L, "ame_debug_read_rt"):
+                L.ame_debug_read_rt.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+                mrt = (ctypes.c_ulonglong * (16 * 32))()
+                wrt = (ctypes.c_ulonglong * (16 * 8))()
+                if L.ame_debug_read_rt(mrt, wrt) == 0:
+                    # main step i = I0 + k: phase-2 start (stamp 1) and gather(i+1) done
+                    # (stamp 24); worker partial m = i + 1 stored: wrt[(i + 1 - I0 - 4) * 8 + 4]
+                    lead, gwait = [], []
+                    for k in range(3, 16):
+                        wi = (k + 1 - 4) * 8 + 4
+                        if mrt[k * 32 + 1] and wrt[wi]:
+                            lead.append((mrt[k * 32 + 1] - wrt[wi]) * 10.0)        # ns
+                            gwait.append((mrt[k * 32 + 24] - mrt[k * 32 + 1]) * 10.0)
+                    if lead:
+                        print(f"    main phase-2 start of step m-1 minus partial m stored (ns, >0: "
+                              f"ready early): median {sorted(lead)[len(lead) // 2]:.0f}, "
+                              f"min {min(lead):.0f}, max {max(lead):.0f}")
+                        print(f"    main gather(m) done minus phase-2 start (ns): median "
+                              f"{sorted(gwait)[len(gwait) // 2]:.0f}")
 
 
 if __name__ == "__main__":
