@@ -12,6 +12,10 @@ def test_options_are_explicit():
     assert EngineOptions.coerce(o) is o
     with pytest.raises(ValueError, match="unknown engine option"):
         EngineOptions.coerce({"spec_dpeth": 3})
+    # the ELBO-beside-the-sweep split is opt-in (0: off; the engine checks the
+    # kernel and the CU count when it is built, tests/test_gpu_w6_workers.py)
+    assert EngineOptions().elbo_cus == 0
+    assert EngineOptions.coerce({"elbo_cus": 32, "sweep_kernel": 24}).elbo_cus == 32
 
 
 def test_queue_depth_model():
