@@ -103,6 +103,9 @@ extern "C" int ame_debug_read_stamps3(unsigned long long* st, unsigned long long
 
 namespace {
 
+#ifndef AME_S3_MOLD_EARLY
+#define AME_S3_MOLD_EARLY 1
+#endif
 constexpr int kNT = 512;    // threads per workgroup
 constexpr int kNH = 448;    // helper lanes
 // Node j of the slice's GEMV belongs to helper lane (j + kGOFF) % 448, slot
@@ -755,6 +758,12 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             const double* mupd = mu64 + ppar * D;     // mu_{i-1} (fp64)
             const double msk = kl ? 1.0 : 0.0;
             const double g = msk * g64[par * D + kc];
+#if AME_S3_MOLD_EARLY
+            // node i's old mean for the publish's damping, read with this step's
+            // first LDS reads (its ring slot was loaded three steps ahead) instead
+            // of a dependent LDS round trip in the publish
+            const float mold_pf = xring[(i & 7) * 64 + kc];
+#endif
             double J0, J1;
             jcol<R>(mup, has_prev && kl, kc, J0, J1);
             // kj = B J^T (the one critical matvec)
@@ -870,8 +879,12 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             // ---- publish ----
             float mold = 0.f, nw = 0.f;
             if (kl) {
+#if AME_S3_MOLD_EARLY
+                mold = mold_pf;
+#else
                 const float* xold = xring + (i & 7) * 64;
                 mold = xold[k];
+#endif
                 nw = mul_add_rn(lr, (float)mus, om, mold);
                 xn[(size_t)i * D + k] = nw;
                 const uint64_t gr = ((uint64_t)a.epoch << 32) | (uint64_t)__float_as_uint(nw);
