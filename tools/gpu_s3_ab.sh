@@ -12,7 +12,7 @@ export PYTHONUNBUFFERED=1
 HB=$!
 timeout -k 10 900 python -u -m pytest -x -q --timeout 600 --timeout-method thread -p no:cacheprovider -m gpu \
     tests/test_gpu_parity.py tests/test_gpu_symmetry.py tests/test_gpu_stale_epoch.py > $OUT/pytest_v3.log 2>&1 &&
-timeout -k 10 900 python -u tools/ab_v3.py tools/_lib/libame_amd_s3m0.so tools/_lib/libame_amd_s3m1.so \
+timeout -k 10 900 python -u tools/ab_v3.py ${S3_LIBS:-tools/_lib/libame_amd_s3m0.so tools/_lib/libame_amd_s3m1.so} \
     --rounds 5 -- --steps 30 --warmup 3 > $OUT/ab_c3.txt 2>&1
 rc=$?
 kill $HB
