@@ -446,6 +446,9 @@ def main():
     ap.add_argument("--elbo-cus", type=int, default=0,
                     help="run the ELBO kernels on a CU-masked stream over this many CUs beside "
                          "the sweep (engine option elbo_cus; needs --sweep-kernel 22 or 24)")
+    ap.add_argument("--elbo-first", choices=("auto", "on", "off"), default="auto",
+                    help="queue each iteration's ELBO before the speculative next sweep (engine "
+                         "option elbo_first; auto = the engine default, off)")
     ap.add_argument("--config5-full", action="store_true",
                     help="BASELINE config 5's own workload (n=4096, T=256, r=32) three-way on "
                          "this one GPU; prints its own JSON line instead of the metric")
@@ -468,6 +471,8 @@ def main():
             c5opts = dict(c5opts or {}, elbo_cus=args.elbo_cus)
         if args.no_pipeline:
             c5opts = dict(c5opts or {}, pipeline=False)
+        if args.elbo_first != "auto":
+            c5opts = dict(c5opts or {}, elbo_first=args.elbo_first == "on")
         out = config5_full(dev, steps=args.steps if args.steps != 50 else 3,
                            warmup=args.warmup if args.warmup != 3 else 1, opts=c5opts)
         print(json.dumps(out), file=json_out, flush=True)
@@ -487,6 +492,8 @@ def main():
         opts["sweep_kernel"] = args.sweep_kernel
     if args.elbo_cus:
         opts["elbo_cus"] = args.elbo_cus
+    if args.elbo_first != "auto":
+        opts["elbo_first"] = args.elbo_first == "on"
     opts = opts or None
     if args.variant == "naive":
         vi = TemporalAMENaiveMFVI(model, learning_rate=args.lr, device=dev,
@@ -612,7 +619,8 @@ def main():
                                   "per slice")},
             "kernels": kernels,
             "schedule": {"pipelined": pipelined,
-                         "sweeps_queued_ahead": int(getattr(eng, "spec_depth", 1))},
+                         "sweeps_queued_ahead": int(getattr(eng, "spec_depth", 1)),
+                         "elbo_first": bool(getattr(eng, "elbo_first", False))},
             "per_rank_ms_per_step": per_rank_ms,
             "scaling_model": scaling_model(n, T_total, world, int(getattr(eng, "spec_depth", 1)),
                                            pipelined),

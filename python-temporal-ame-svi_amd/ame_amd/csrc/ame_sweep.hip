@@ -109,11 +109,35 @@ extern "C" int ame_debug_read_wstamps(unsigned long long* host) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ame_wstamps), sizeof(g_ame_wstamps), 0,
                                hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
+// wavefront lag: s_memrealtime at the start of steps AME_STAMP_I0,
+// AME_STAMP_I0 + 64 and 0 on thread 0 of every slice (local slice < 64); slots
+// 3-5: prologue marks (LAGMARK)
+__device__ unsigned long long g_ame_lag[64 * 8];
+extern "C" int ame_debug_read_lag(unsigned long long* host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ame_lag), sizeof(g_ame_lag), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#define LAGMARK(tl_, slot)                                                                 \
+    do {                                                                                   \
+        if ((tl_) < 64) {                                                                  \
+            unsigned long long r_;                                                         \
+            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r_)::"memory"); \
+            g_ame_lag[(tl_) * 8 + (slot)] = r_;                                            \
+        }                                                                                  \
+    } while (0)
+// s_memrealtime at kernel entry of every workgroup (blockIdx < 512), and its
+// hardware placement (HW_ID: CU / SE / XCC bits)
+__device__ unsigned long long g_ame_entry[512 * 2];
+extern "C" int ame_debug_read_entry(unsigned long long* host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ame_entry), sizeof(g_ame_entry), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
 extern "C" int ame_debug_read_stamps(unsigned long long* host, int count) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ame_stamps), sizeof(unsigned long long) * count,
                                0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #else
+#define LAGMARK(tl_, slot) do { } while (0)
 #define WSTAMP(ph) do { } while (0)
 #define P2STAMP(sl) do { } while (0)
 #define STAMP(ph) \
@@ -395,6 +419,7 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
         }
     };
     y_prefetch(0);
+    if (g == 0 && tid == 0) LAGMARK(t, 6);
     for (int m = 0; m < n; ++m) {
         WSTAMP(0);
         // node m-4's new mean replaces its old one (owner wave); every worker
@@ -513,6 +538,7 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
             gran_store_agent(hp + (size_t)(m % AME_GW_RING) * PW + tid,
                              ((uint64_t)tag << 32) | (uint64_t)__float_as_uint(v));
         }
+        if (m == 0 && g == 0 && tid == 0) LAGMARK(t, 5);
         WSTAMP(4);
     }
 }
@@ -579,6 +605,17 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     constexpr int NLT = D * (D + 1) / 2, LTQ = (NLT + AME_NT - 1) / AME_NT;
     const int n = dm.n, TL = dm.T_local, Tt = dm.T_total;
     extern __shared__ __attribute__((aligned(16))) char smem[];
+#ifdef AME_STAMPS
+    if (threadIdx.x == 0 && blockIdx.x < 512) {
+        unsigned long long r_;
+        unsigned int hw_, xcc_;
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r_)::"memory");
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));
+        g_ame_entry[blockIdx.x * 2] = r_;
+        g_ame_entry[blockIdx.x * 2 + 1] = ((unsigned long long)xcc_ << 32) | hw_;
+    }
+#endif
     int slice = blockIdx.x, role = 0;
     if constexpr (WK) {
         v2_block_role<MODE>(TL, slice, role);
@@ -674,40 +711,110 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     if (tid < D) pcd[tid] = pconst_entry(a.consts, D, tid, tid, tg, Tt);
     if (tid == 0) wsync[0] = wsync[1] = 0u;
     __syncthreads();
-    if (tid < M2) {   // sum of squares over all nodes: ssq[c<R] = sum U_c^2, ssq[R+c] = sum V_c^2
-        double acc = 0.0;
-        for (int j = 0; j < n; ++j) {
-            const double v = (double)mold(j)[tid];
-            acc = fma(v, v, acc);
-        }
-        ssq[tid] = acc;
-    }
-    for (int e = tid; e < NLT; e += AME_NT) {
-        int k, m;
-        tri_decode(e, k, m);
+    // entry (k, m) of P_0 from its node sum (k >= 2: sum of U/V entries, or of
+    // products of two); k < 2 rows are constants times n - 1
+    auto p0_entry = [&](int k, int m, double acc) -> double {
         double v;
         if (k < 2) {
             v = ((k == 0 && m == 0) ? p : (k == 1 && m == 1) ? s : q) * (double)(n - 1);
         } else {
-            const int ck = k - 2;
-            const bool ku = ck < R;                 // row U_ck: J entry V ; row V: J entry U
-            const int kc = ku ? R + ck : ck - R;
-            double acc = 0.0;
+            const bool ku = k - 2 < R;
             if (m < 2) {
-                for (int j = 1; j < n; ++j) acc += (double)mold(j)[kc];
                 v = (ku ? (m == 0 ? p : q) : (m == 0 ? q : s)) * acc;
             } else {
-                const int cm = m - 2;
-                const bool mu_ = cm < R;
-                const int mc = mu_ ? R + cm : cm - R;
-                for (int j = 1; j < n; ++j)
-                    acc = fma((double)mold(j)[kc], (double)mold(j)[mc], acc);
+                const bool mu_ = m - 2 < R;
                 v = ((ku && mu_) ? p : ((!ku && !mu_) ? s : q)) * acc;
             }
         }
-        v += pconst_entry(a.consts, D, k, m, tg, Tt);
-        K[k * KS + m] = v;
-        K[m * KS + k] = v;
+        return v + pconst_entry(a.consts, D, k, m, tg, Tt);
+    };
+    // the U/V column of row k (k >= 2) that J carries: row U_c has entry V_c, row V_c entry U_c
+    auto jcol = [&](int k) { const int ck = k - 2; return ck < R ? R + ck : ck - R; };
+    if constexpr (MG || WK) {
+        // The old (U,V) rows live in HBM here: staged through LDS in chunks of CH
+        // rows (cst is free until phase 3 of step 0).  Every entry keeps its own
+        // accumulator and adds the nodes in order, as the direct form below does
+        // (the same operations, the same roundings); the direct form made one
+        // dependent HBM / L2 round trip per node and entry -- at config 5's rank
+        // shape the prologue took ~2 200 node steps of the sweep
+        // (profiles/r05_c5_prologue_stamps.txt).
+        constexpr int CH = (D * D) / M2;
+        constexpr int NLQ = (NLT + AME_NT - 1) / AME_NT;
+        float* xs = cst;
+        double acc[NLQ];
+#pragma unroll
+        for (int qq = 0; qq < NLQ; ++qq) acc[qq] = 0.0;
+        double sq = 0.0;
+        for (int j0 = 0; j0 < n; j0 += CH) {
+            const int nc = min(CH, n - j0);
+            __syncthreads();
+            for (int e = tid; e < nc * M2; e += AME_NT) {
+                const int jj = e / M2, c = e - jj * M2;
+                xs[e] = xo[(size_t)(j0 + jj) * D + 2 + c];
+            }
+            __syncthreads();
+            if (tid < M2) {   // sum of squares over all nodes (ssq)
+                for (int jj = 0; jj < nc; ++jj) {
+                    const double v = (double)xs[jj * M2 + tid];
+                    sq = fma(v, v, sq);
+                }
+            }
+            const int js = (j0 == 0) ? 1 : 0;   // node 0 is not in P_0's sums
+#pragma unroll
+            for (int qq = 0; qq < NLQ; ++qq) {
+                const int e = tid + AME_NT * qq;
+                if (e >= NLT) continue;
+                int k, m;
+                tri_decode(e, k, m);
+                if (k < 2) continue;
+                const int kc = jcol(k);
+                if (m < 2) {
+                    for (int jj = js; jj < nc; ++jj) acc[qq] += (double)xs[jj * M2 + kc];
+                } else {
+                    const int mc = jcol(m);
+                    for (int jj = js; jj < nc; ++jj)
+                        acc[qq] = fma((double)xs[jj * M2 + kc], (double)xs[jj * M2 + mc], acc[qq]);
+                }
+            }
+        }
+        if (tid < M2) ssq[tid] = sq;
+#pragma unroll
+        for (int qq = 0; qq < NLQ; ++qq) {
+            const int e = tid + AME_NT * qq;
+            if (e >= NLT) continue;
+            int k, m;
+            tri_decode(e, k, m);
+            const double v = p0_entry(k, m, acc[qq]);
+            K[k * KS + m] = v;
+            K[m * KS + k] = v;
+        }
+    } else {
+        if (tid < M2) {   // sum of squares over all nodes: ssq[c<R] = sum U_c^2, ssq[R+c] = sum V_c^2
+            double acc = 0.0;
+            for (int j = 0; j < n; ++j) {
+                const double v = (double)mold(j)[tid];
+                acc = fma(v, v, acc);
+            }
+            ssq[tid] = acc;
+        }
+        for (int e = tid; e < NLT; e += AME_NT) {
+            int k, m;
+            tri_decode(e, k, m);
+            double acc = 0.0;
+            if (k >= 2) {
+                const int kc = jcol(k);
+                if (m < 2) {
+                    for (int j = 1; j < n; ++j) acc += (double)mold(j)[kc];
+                } else {
+                    const int mc = jcol(m);
+                    for (int j = 1; j < n; ++j)
+                        acc = fma((double)mold(j)[kc], (double)mold(j)[mc], acc);
+                }
+            }
+            const double v = p0_entry(k, m, acc);
+            K[k * KS + m] = v;
+            K[m * KS + k] = v;
+        }
     }
     __syncthreads();
     for (int pv = 0; pv < D; ++pv) {   // in-place symmetric sweep: K -> -P_0^-1
@@ -1155,6 +1262,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 uint64_t g0[KH];
                 first_poll(0, g0);
                 poll_left(0, g0);
+                if (lane == 0) LAGMARK(tl, 3);
             } else {
                 zero_left();
             }
@@ -1183,6 +1291,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     // which the gather above has seen: acquire them for the whole workgroup
     if constexpr (WK) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     gemv_reduce(0);
+    if (tid == 0) LAGMARK(tl, 4);
     if constexpr (WK) ar_left_finish(0, ar_right_load(0));
     else ar_terms(0);
     __syncthreads();
@@ -1195,6 +1304,11 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     for (int i = 0; i < n; ++i) {
 #ifdef AME_STAMPS
         const bool stamp_on = (tl == TL / 2) && i >= AME_STAMP_I0 && i < AME_STAMP_I0 + 16;
+        if (tid == 0 && tl < 64 && (i == AME_STAMP_I0 || i == AME_STAMP_I0 + 64 || i == 0)) {
+            unsigned long long r_;
+            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r_)::"memory");
+            g_ame_lag[tl * 8 + (i == 0 ? 2 : (i != AME_STAMP_I0))] = r_;
+        }
 #endif
         STAMP(0);
         const bool has_prev = i > 0, has_next = i + 1 < n;

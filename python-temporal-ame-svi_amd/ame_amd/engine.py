@@ -87,6 +87,11 @@ class EngineOptions:
                   Needs a non-pipelined GEMV-worker kind (sweep_kernel 22 or 24)
                   whose launch fits the remaining CUs (kind 24 at config 5's
                   rank shape: 32 slices x 7 workgroups = 224 CUs, elbo_cus 32)
+    elbo_first    queue this iteration's ELBO kernels before the speculative
+                  next sweep and order that sweep after them (default: after
+                  it).  Same results; measured at config 5's rank shape (kind
+                  22) no faster: 32.8-35.5 vs 33.0-34.0 ms per iteration
+                  (profiles/r05_c5_elbo_first_ab.txt), so off
     """
     sweep_kernel: int = 0
     pipeline: bool = True
@@ -95,6 +100,7 @@ class EngineOptions:
     slice_group: int = 0
     pairs_kernel: int = 0
     elbo_cus: int = 0
+    elbo_first: bool = False
 
     @classmethod
     def coerce(cls, opts) -> "EngineOptions":
@@ -402,6 +408,10 @@ class DeviceEngine:
             # with more than one queued that is a serial chain anyway, so the
             # queue is one deep (_launch_sweep also orders after the last one).
             self.spec_depth = 1
+        # ELBO before the speculative sweep (EngineOptions.elbo_first)
+        self.elbo_first = bool(opt.elbo_first)
+        if self.halo is not None:   # the collectives of sums() keep one order on every rank
+            self.elbo_first = self.halo.agree(self, self.elbo_first)
         # scratch per launch; pipelined, two launches run at once: two halves
         self._work_half = sws
         with torch.cuda.device(dev):
@@ -691,9 +701,15 @@ class DeviceEngine:
         speculate=k > 0 (iterations still to come) up to k next sweeps are
         started first and run beside them."""
         if not self._out_valid:
-            if speculate:
-                self.speculate(int(speculate))
-            self.launch_elbo()
+            if self.elbo_first:
+                # the sweep's `ready` event (main stream) then follows the ELBO
+                self.launch_elbo()
+                if speculate:
+                    self.speculate(int(speculate))
+            else:
+                if speculate:
+                    self.speculate(int(speculate))
+                self.launch_elbo()
             out = self.out
             if self.halo is not None:
                 out = self.halo.allreduce_sums(out)

@@ -16,6 +16,10 @@ def test_options_are_explicit():
     # kernel and the CU count when it is built, tests/test_gpu_w6_workers.py)
     assert EngineOptions().elbo_cus == 0
     assert EngineOptions.coerce({"elbo_cus": 32, "sweep_kernel": 24}).elbo_cus == 32
+    # ELBO-before-the-speculative-sweep: opt-in, measured no faster
+    # (tests/test_gpu_w6_workers.py::test_elbo_first_bit_equal)
+    assert EngineOptions().elbo_first is False
+    assert EngineOptions.coerce({"elbo_first": True}).elbo_first is True
 
 
 def test_queue_depth_model():

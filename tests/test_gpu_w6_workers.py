@@ -14,7 +14,9 @@ wave holding 176 nodes (152 in registers, 24 in LDS).  Checks:
 * elbo_cus: the ELBO kernels on CUs [0, 32), the sweep on the other 224 --
   the fit (means, covariances, every iteration's ELBO and MSE) bit for bit
   the single-stream run, at config 5's rank shape and at a small shape;
-  bad CU ranges and kinds are refused.
+  bad CU ranges and kinds are refused;
+* elbo_first (opt-in: the ELBO queued before the speculative sweep): bit for
+  bit the default sweep-first order.
 
 Reference: structured_mf.py:211-326, naive_mf.py:207-282, temporal_ame.py:255-291.
 """
@@ -91,6 +93,24 @@ def test_elbo_cus_small_bit_equal(n, T, r, method, iters, gpu_device):
     _, d = _fit(n, T, r, method, 0.4, gpu_device, iters, 5, sweep_kernel=_lib.AME_SWEEP_V2_WORKERS)
     for x, y in zip(c, d):
         assert np.array_equal(np.asarray(x), np.asarray(y))
+
+
+@pytest.mark.parametrize("n,T,r,method,iters", [(300, 6, 32, "good", 4), (200, 5, 24, "naive", 3)])
+def test_elbo_first_bit_equal(n, T, r, method, iters, gpu_device):
+    """The ELBO queued before the speculative sweep (elbo_first, opt-in)
+    changes only the launch order: the fit bit for bit the default sweep-first
+    order, for kind 22 and kind 24."""
+    from ame_amd import _lib
+    for kind in (_lib.AME_SWEEP_V2_WORKERS, W6):
+        eng, a = _fit(n, T, r, method, 0.4, gpu_device, iters, 7, sweep_kernel=kind,
+                      elbo_first=True)
+        assert eng.elbo_first and eng.sweep_kind == kind
+        del eng
+        eng, b = _fit(n, T, r, method, 0.4, gpu_device, iters, 7, sweep_kernel=kind)
+        assert not eng.elbo_first
+        del eng
+        for x, y in zip(a, b):
+            assert np.array_equal(np.asarray(x), np.asarray(y))
 
 
 def test_elbo_cus_refused(gpu_device):

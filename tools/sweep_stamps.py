@@ -16,6 +16,7 @@ PKG = os.path.join(ROOT, "python-temporal-ame-svi_amd")
 BDIR = os.path.join(PKG, "ame_amd", "_build")      # objects (not shipped to the GPU box)
 LIBDIR = os.path.join(ROOT, "tools", "_lib")         # variant libraries (shipped)
 SO = os.path.join(LIBDIR, "libame_amd_stamps.so")
+AME_STAMP_I0 = 256   # ame_sweep.hip
 PHASES = ["phase 1: K-matvecs + z staging", "phase 2: wave0 Woodbury | waves1-3 GEMV+poll",
           "phase 3: K rank-4 update + cov write + AR", "loop (+ cov prefetch issue)"]
 
@@ -159,6 +160,53 @@ def run():
                               f"min {min(lead):.0f}, max {max(lead):.0f}")
                         print(f"    main gather(m) done minus phase-2 start (ns): median "
                               f"{sorted(gwait)[len(gwait) // 2]:.0f}")
+    if hasattr(L, "ame_debug_read_lag"):   # wavefront lag between consecutive slices
+        L.ame_debug_read_lag.argtypes = [ctypes.c_void_p]
+        lb = (ctypes.c_ulonglong * 512)()
+        TL = min(vi.engine.groups[0][1], 64)   # (offset, size) of the one group
+        if L.ame_debug_read_lag(lb) == 0 and lb[0]:
+            s0 = [lb[8 * t] for t in range(TL)]
+            s1 = [lb[8 * t + 1] for t in range(TL)]
+            st = [lb[8 * t + 2] for t in range(TL)]
+            per = sorted((s1[t] - s0[t]) * 10.0 / 64 for t in range(TL))      # ns per step
+            lag = sorted((s0[t] - s0[t - 1]) * 10.0 for t in range(1, TL))    # ns
+            p = per[len(per) // 2]
+            print(f"wavefront: node period {p:.0f} ns (median over {TL} slices, steps "
+                  f"{AME_STAMP_I0}..{AME_STAMP_I0 + 64}); slice-to-slice lag at step {AME_STAMP_I0}: "
+                  f"median {lag[len(lag) // 2]:.0f} ns = {lag[len(lag) // 2] / p:.2f} steps, "
+                  f"min {lag[0] / p:.2f}, max {lag[-1] / p:.2f}; last slice - first slice "
+                  f"{(s0[-1] - s0[0]) * 10.0 / p:.1f} steps over {TL - 1} hops")
+            t0 = min(st)
+            print("  per slice (steps of that period, from the earliest step-0 start): step 0 at / "
+                  f"step {AME_STAMP_I0} at")
+            eb = None
+            if hasattr(L, "ame_debug_read_entry"):
+                L.ame_debug_read_entry.argtypes = [ctypes.c_void_p]
+                eb = (ctypes.c_ulonglong * 1024)()
+                if L.ame_debug_read_entry(eb) != 0 or not eb[0]:
+                    eb = None
+            NG = {_lib.AME_SWEEP_V2_WORKERS: 7, _lib.AME_SWEEP_V2_W6: 6}.get(vi.engine.sweep_kind, 0)
+            if eb is not None:
+                nb = TL * (1 + NG)
+                e0 = min(eb[2 * b] for b in range(nb))
+                print("  workgroup entry (kernel start), steps after the first workgroup's entry; "
+                      "main workgroup / last of its workers; then step 0 / step 256 from the earliest step 0")
+            for t in range(TL):
+                extra = ""
+                if eb is not None:
+                    me = (eb[2 * t] - e0) * 10.0 / p
+                    ws = [TL + NG * t + w for w in range(NG)]
+                    we = max((eb[2 * b] - e0) * 10.0 / p for b in ws) if ws else 0.0
+                    hid = eb[2 * t + 1]
+                    mk = [(lb[8 * t + j] - e0) * 10.0 / p if lb[8 * t + j] else float("nan")
+                          for j in (6, 5, 3, 4, 2)]
+                    extra = (f"   entry {me:6.1f} / {we:6.1f}  w0 loop {mk[0]:7.1f}  w0 part0 {mk[1]:7.1f}"
+                             f"  left0 {mk[2]:7.1f}  gather0 {mk[3]:7.1f}  step0 {mk[4]:7.1f}"
+                             f"  xcc {hid >> 32}")
+                print(f"    slice {t:3d}: {(st[t] - t0) * 10.0 / p:8.1f}  {(s0[t] - t0) * 10.0 / p:8.1f}{extra}")
+            if eb is not None:
+                late = sorted(((eb[2 * b] - e0) * 10.0 / p, b) for b in range(nb))[-6:]
+                print("  latest workgroup entries (steps, blockIdx):", [(round(x, 1), b) for x, b in late])
 
 
 if __name__ == "__main__":
