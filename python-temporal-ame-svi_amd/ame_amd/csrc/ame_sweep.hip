@@ -816,6 +816,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             K[m * KS + k] = v;
         }
     }
+    if (tid == 0 && tg == 0) LAGMARK(tl, 3);   // slice 0 has no left poll (slot 3)
     __syncthreads();
     for (int pv = 0; pv < D; ++pv) {   // in-place symmetric sweep: K -> -P_0^-1
         if (tid < D) red[tid] = K[pv * KS + tid];
@@ -838,6 +839,7 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         const int k = e / D, m = e - k * D;
         K[k * KS + m] = -K[k * KS + m];
     }
+    if (tid == 0) LAGMARK(tl, 7);
 
     const int at = WK ? tid - 64 : tid;   // AR thread index
     // AR rows: thread (k = at / NPA, part = at % NPA); WK reads the PhiTQi half

@@ -199,9 +199,10 @@ def run():
                     we = max((eb[2 * b] - e0) * 10.0 / p for b in ws) if ws else 0.0
                     hid = eb[2 * t + 1]
                     mk = [(lb[8 * t + j] - e0) * 10.0 / p if lb[8 * t + j] else float("nan")
-                          for j in (6, 5, 3, 4, 2)]
+                          for j in (6, 5, 3, 7, 4, 2)]
                     extra = (f"   entry {me:6.1f} / {we:6.1f}  w0 loop {mk[0]:7.1f}  w0 part0 {mk[1]:7.1f}"
-                             f"  left0 {mk[2]:7.1f}  gather0 {mk[3]:7.1f}  step0 {mk[4]:7.1f}"
+                             f"  left0|sums {mk[2]:7.1f}  P0inv {mk[3]:7.1f}  gather0 {mk[4]:7.1f}"
+                             f"  step0 {mk[5]:7.1f}"
                              f"  xcc {hid >> 32}")
                 print(f"    slice {t:3d}: {(st[t] - t0) * 10.0 / p:8.1f}  {(s0[t] - t0) * 10.0 / p:8.1f}{extra}")
             if eb is not None:
