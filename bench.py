@@ -252,8 +252,13 @@ def load_pmc(tag):
 
 
 # node steps of wavefront lag per slice of the in-order GEMV-worker sweep (kind
-# 22): profiles/r05_*_c5_fill.jsonl (iteration time at T_local = 32 vs 1)
-FILL_STEPS_KIND22 = 3.0
+# 22), measured directly: slice-to-slice start lag at step 256, median over the
+# 31 hops of config 5's rank shape, 1.26-1.46 in nine stamped runs
+# (s_memrealtime on every slice; profiles/r05_c5_lag_stamps.txt,
+# r05_c5_prologue_stamps.txt), rounded up.  (Round 5 first used 3.0 from whole
+# iteration times at T_local = 32 vs 1, profiles/r05_d_c5_fill.jsonl, which
+# also carry the per-launch prologue and the per-step cost of a fuller chip.)
+FILL_STEPS_KIND22 = 1.5
 
 
 def scaling_model(n, T_total, world, depth, pipelined, fill=None):
