@@ -741,9 +741,32 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         constexpr int CH = (D * D) / M2;
         constexpr int NLQ = (NLT + AME_NT - 1) / AME_NT;
         float* xs = cst;
+        // this thread's entries: the two U/V columns each reads (column 0 for an
+        // entry that takes no part) and the entry's kind; node-outer and
+        // branch-free below, so the entries' LDS reads batch and their fp64
+        // chains interleave -- each still adds its nodes in order with the
+        // direct form's operations (same roundings)
         double acc[NLQ];
+        int ekc[NLQ], emc[NLQ];
+        bool live[NLQ], plain[NLQ];
 #pragma unroll
-        for (int qq = 0; qq < NLQ; ++qq) acc[qq] = 0.0;
+        for (int qq = 0; qq < NLQ; ++qq) {
+            acc[qq] = 0.0;
+            ekc[qq] = emc[qq] = 0;
+            live[qq] = plain[qq] = false;
+            const int e = tid + AME_NT * qq;
+            if (e < NLT) {
+                int k, m;
+                tri_decode(e, k, m);
+                if (k >= 2) {
+                    live[qq] = true;
+                    ekc[qq] = jcol(k);
+                    plain[qq] = m < 2;
+                    emc[qq] = (m < 2) ? ekc[qq] : jcol(m);
+                }
+            }
+        }
+        const int sc = (tid < M2) ? tid : 0;
         double sq = 0.0;
         for (int j0 = 0; j0 < n; j0 += CH) {
             const int nc = min(CH, n - j0);
@@ -753,27 +776,27 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 xs[e] = xo[(size_t)(j0 + jj) * D + 2 + c];
             }
             __syncthreads();
-            if (tid < M2) {   // sum of squares over all nodes (ssq)
-                for (int jj = 0; jj < nc; ++jj) {
-                    const double v = (double)xs[jj * M2 + tid];
-                    sq = fma(v, v, sq);
-                }
+            int js = 0;
+            if (j0 == 0) {   // node 0: in the sums of squares only
+                const double v = (double)xs[sc];
+                sq = fma(v, v, sq);
+                js = 1;
             }
-            const int js = (j0 == 0) ? 1 : 0;   // node 0 is not in P_0's sums
+            for (int jj = js; jj < nc; ++jj) {
+                const float* row = xs + jj * M2;
+                float xk[NLQ], xm[NLQ];
+                const float xs2 = row[sc];
 #pragma unroll
-            for (int qq = 0; qq < NLQ; ++qq) {
-                const int e = tid + AME_NT * qq;
-                if (e >= NLT) continue;
-                int k, m;
-                tri_decode(e, k, m);
-                if (k < 2) continue;
-                const int kc = jcol(k);
-                if (m < 2) {
-                    for (int jj = js; jj < nc; ++jj) acc[qq] += (double)xs[jj * M2 + kc];
-                } else {
-                    const int mc = jcol(m);
-                    for (int jj = js; jj < nc; ++jj)
-                        acc[qq] = fma((double)xs[jj * M2 + kc], (double)xs[jj * M2 + mc], acc[qq]);
+                for (int qq = 0; qq < NLQ; ++qq) {
+                    xk[qq] = row[ekc[qq]];
+                    xm[qq] = row[emc[qq]];
+                }
+                sq = fma((double)xs2, (double)xs2, sq);
+#pragma unroll
+                for (int qq = 0; qq < NLQ; ++qq) {
+                    const double a_ = (double)xk[qq], b_ = (double)xm[qq];
+                    const double nv = plain[qq] ? acc[qq] + a_ : fma(a_, b_, acc[qq]);
+                    acc[qq] = live[qq] ? nv : acc[qq];
                 }
             }
         }

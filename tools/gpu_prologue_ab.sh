@@ -22,7 +22,7 @@ for cfg in "600,8,32 good 3 22" "600,8,32 naive 3 22" "600,8,32 bad 3 22" "1024,
 done
 if [ $rc -eq 0 ]; then
     timeout -k 10 300 python -u tools/sweep_stamps.py --tag=c5lag --n=4096 --T=32 --r=32 --kind=22 > $OUT/stamps.txt 2>&1 &&
-    timeout -k 10 600 python -u tools/ab_v3.py $OLD $NEW --rounds 3 -- \
+    timeout -k 10 600 python -u tools/ab_v3.py $OLD ${MID:+$MID} $NEW --rounds ${ROUNDS:-3} -- \
         --n 4096 --t-per-gpu 32 --latent-dim 32 --steps 10 --warmup 2 --no-secondary > $OUT/ab.txt 2>&1 &&
     timeout -k 10 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread -p no:cacheprovider \
         -m gpu tests/test_gpu_w6_workers.py > $OUT/pytest_w6.log 2>&1
