@@ -518,16 +518,24 @@ def main():
         torch.cuda.synchronize(dev)
 
     barrier()
+    # device-side cross-rank wait time (status words 11 / 12, microseconds summed
+    # over sweeps; include/ame_amd.h): read before and after the timed region
+    cw0 = eng.status[11:13].cpu().tolist()
     t0 = time.perf_counter()
     hist = vi.fit(max_iter=args.steps, tolerance=0.0, verbose=False)
     barrier()
     dt = time.perf_counter() - t0
+    cw1 = eng.status[11:13].cpu().tolist()
+    cross_ms = [((b - a) & 0xFFFFFFFF) / 1e3 / args.steps for a, b in zip(cw0, cw1)]
     per_rank_ms = [dt / args.steps * 1e3]
+    per_rank_cross = [cross_ms]
     if use_dist:
-        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        tt = torch.tensor([dt, cross_ms[0], cross_ms[1]], dtype=torch.float64, device=dev)
         allt = [torch.zeros_like(tt) for _ in range(world)]
         dist.all_gather(allt, tt)
-        per_rank_ms = [float(x.item()) / args.steps * 1e3 for x in allt]
+        per_rank_ms = [float(x[0].item()) / args.steps * 1e3 for x in allt]
+        per_rank_cross = [[float(x[1].item()), float(x[2].item())] for x in allt]
+        tt = tt[:1].clone()
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     kms, kcount = eng.kernel_ms()
@@ -627,6 +635,11 @@ def main():
                          "sweeps_queued_ahead": int(getattr(eng, "spec_depth", 1)),
                          "elbo_first": bool(getattr(eng, "elbo_first", False))},
             "per_rank_ms_per_step": per_rank_ms,
+            "per_rank_cross_wait_ms_per_step": {
+                "halo": [c[0] for c in per_rank_cross], "back": [c[1] for c in per_rank_cross],
+                "note": ("device-side time per fit() iteration that the rank's first slice spun on "
+                         "the left rank's hand-off granules (halo) and its last slice on the right "
+                         "rank's back channel (status words 11 / 12, s_memrealtime); 0 on one GPU")},
             "scaling_model": scaling_model(n, T_total, world, int(getattr(eng, "spec_depth", 1)),
                                            pipelined),
             "build": _lib_provenance(),

@@ -60,6 +60,37 @@ enum ame_variant { AME_GOOD = 0, AME_BAD = 1, AME_NAIVE = 2 };
  * unordered host write; the word is not consumed as if it were current */
 #define AME_STATUS_STALE_EPOCH 8u
 
+/* The status block: AME_STATUS_WORDS uint32 words (the caller zeroes it once
+ * and again after reading a failure).
+ *   [0]  AME_STATUS_* bits
+ *   [1]  1 once the FIRST failing wait has written its record into [2..8]
+ *   [2]  wait site (enum ame_wait_site)     [3] global time slice of the waiter
+ *   [4]  node index (0xFFFFFFFF: before the node loop)
+ *   [5]  word observed (epoch tag, done value, LDS count)   [6] value expected
+ *   [7]  microseconds waited                [8] the sweep's epoch
+ *   [9]  device bookkeeping: workgroups inside a cross-rank wait right now
+ *   [10] waits that gave up quietly because [0] was already non-zero
+ *   [11] microseconds the rank's first slice spun on the left rank's granules
+ *   [12] microseconds its last slice spun on the right rank's back channel
+ *        ([11], [12] accumulate over sweeps; the caller reads differences)
+ * Wait rules (every kernel that spins): a wait gives up quietly -- no bit of its
+ * own -- once [0] is non-zero (one failure does not manufacture more); a wait
+ * on this GPU (slice -> slice, done flags, LDS counters) restarts its 2 s
+ * budget while [9] > 0, since its producer may then sit behind a neighbouring
+ * rank, whose own wait has the 10 s budget; a workgroup that failed or gave up
+ * stores no done flag, back channel or current-epoch hand-off granule. */
+#define AME_STATUS_WORDS 16
+enum ame_wait_site {
+    AME_WAIT_DONE_SELF = 1,     /* pipelined prologue: done[t] of the previous sweep */
+    AME_WAIT_DONE_RIGHT = 2,    /* pipelined prologue: done[t+1] (or the next group's first slice) */
+    AME_WAIT_BACK = 3,          /* pipelined prologue: the right rank's back-channel done word */
+    AME_WAIT_GRAN_LOCAL = 4,    /* hand-off granule of slice t-1 on this GPU */
+    AME_WAIT_GRAN_HALO = 5,     /* hand-off granule of the left rank's last slice */
+    AME_WAIT_LDS = 6,           /* intra-workgroup LDS counter */
+    AME_WAIT_WORKER_GRAN = 7,   /* GEMV worker: new-mean granule of its slice */
+    AME_WAIT_PARTIAL = 8        /* slice workgroup: a GEMV worker's partial */
+};
+
 /* float offset of the done word in a back channel of n*d floats */
 #define AME_BACK_DONE_OFFSET(nd) ((((nd) + 63) / 64) * 64)
 
@@ -132,7 +163,7 @@ typedef struct ame_sweep_args {
     float lr;                    /* learning_rate (damping) */
     float one_minus_lr;          /* (float)(1 - lr) computed in double on the host */
     uint32_t epoch;              /* sweep counter, >= 1, identical on every rank */
-    uint32_t* status;            /* [1] error word */
+    uint32_t* status;            /* [AME_STATUS_WORDS] status block (bits + first-failure record) */
     double* work;                /* scratch, >= ame_sweep_work_size() doubles: 0 for the v3
                                     sweep; the GEMV workers' partial ring (zeroed by the call
                                     itself) and the right-neighbour AR terms (filled by the call)

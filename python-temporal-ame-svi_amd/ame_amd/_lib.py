@@ -17,6 +17,16 @@ AME_STATUS_SPIN_TIMEOUT = 1
 AME_STATUS_HALO_TIMEOUT = 2
 AME_STATUS_LDS_TIMEOUT = 4
 AME_STATUS_STALE_EPOCH = 8
+# the status block (include/ame_amd.h): bits, first-failure record, bookkeeping
+AME_STATUS_WORDS = 16
+AME_WAIT_SITES = {1: "done flag of slice t (previous sweep)",
+                  2: "done flag of slice t+1 (previous sweep)",
+                  3: "back channel of the right rank (previous sweep)",
+                  4: "hand-off granule of slice t-1",
+                  5: "hand-off granule of the left rank's last slice",
+                  6: "LDS counter inside the workgroup",
+                  7: "GEMV worker: new-mean granule of its slice",
+                  8: "slice workgroup: GEMV worker partial"}
 AME_PEER_HANDLE_BYTES = 64
 # sweep kernel requests / kinds (enum ame_sweep_kind_code)
 AME_SWEEP_AUTO, AME_SWEEP_V2_SINGLE, AME_SWEEP_V2_AUTO, AME_SWEEP_V3 = 0, 1, 2, 3
@@ -87,6 +97,9 @@ def _declare(L):
     L.ame_elbo_work_size.restype = ctypes.c_longlong
     L.ame_debug_selftest.argtypes = [c_vp, c_vp]
     L.ame_debug_selftest.restype = ctypes.c_int
+    if hasattr(L, "ame_debug_occupy"):   # diagnostic; absent from older A/B builds
+        L.ame_debug_occupy.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint, c_vp, c_vp]
+        L.ame_debug_occupy.restype = ctypes.c_int
     L.ame_sweep_orders_slices.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
     L.ame_sweep_orders_slices.restype = ctypes.c_int
     L.ame_sweep_kind.argtypes = [P(ame_dims), ctypes.c_int]

@@ -11,6 +11,84 @@
 #define AME_SPIN_TICKS_LOCAL (200ull * 1000 * 1000)   // 2 s, lane -> lane on one GPU
 #define AME_SPIN_TICKS_HALO (1000ull * 1000 * 1000)   // 10 s, rank -> rank
 
+// ---- bounded waits and the status block (include/ame_amd.h) ----
+#define AME_ST_CLAIM 1
+#define AME_ST_CROSS 9    // workgroups inside a cross-rank wait right now
+#define AME_ST_QUIET 10   // waits that gave up quietly after the first failure
+#define AME_ST_HALO_US 11 // microseconds first slices spun on the left rank's granules
+#define AME_ST_BACK_US 12 // microseconds last slices spun on the right rank's back channel
+// node index of a wait before the node loop (prologue)
+#define AME_NODE_NONE 0xFFFFFFFFu
+
+__device__ __forceinline__ uint32_t ame_st_load(uint32_t* st, int w) {
+    return __hip_atomic_load(st + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One lane.  A failure sets its bit unless an earlier one already set a bit
+// (then it only counts a quiet give-up: the first failure is the cause, the
+// rest are its consequences); the first to claim the record fills it.
+__device__ __forceinline__ void ame_fail(uint32_t* st, uint32_t bit, int site, int slice, uint32_t node,
+                                         uint32_t observed, uint32_t expected, uint64_t ticks,
+                                         uint32_t epoch) {
+    if (ame_st_load(st, 0) != 0u) {
+        atomicAdd(st + AME_ST_QUIET, 1u);
+        return;
+    }
+    atomicOr(st, bit);
+    if (atomicCAS(st + AME_ST_CLAIM, 0u, 1u) == 0u) {
+        const uint64_t us = ticks / 100u;
+        st[2] = (uint32_t)site;
+        st[3] = (uint32_t)slice;
+        st[4] = node;
+        st[5] = observed;
+        st[6] = expected;
+        st[7] = (uint32_t)(us > 0xFFFFFFFFull ? 0xFFFFFFFFull : us);
+        st[8] = epoch;
+        __threadfence();
+    }
+}
+
+// The slow path of one bounded wait, run by the waiting wave (or thread):
+//   AmeSpin w(st, cross, leader);  while (!arrived) { switch (w.poll()) ... }  w.end();
+// poll(): 0 keep waiting, 1 give up quietly (the status block already holds a
+// failure), 2 budget spent (the caller reports through ame_fail).  A wait on
+// this GPU restarts its budget while any workgroup sharing the status block is
+// inside a cross-rank wait: its producer may stand behind that rank (no
+// progress is expected until it arrives, and that wait has its own budget).
+// acct (a cross-rank wait's leader only): status word that end() adds the
+// microseconds spent to -- AME_ST_HALO_US / AME_ST_BACK_US, the per-rank halo
+// wait time the bench reports; 0 = none.
+struct AmeSpin {
+    uint32_t* st;
+    uint64_t t_first, t0;
+    bool cross, leader;
+    int acct;
+    __device__ __forceinline__ AmeSpin(uint32_t* s, bool cr, bool ld, int ac = 0)
+        : st(s), cross(cr), leader(ld), acct(ac) {
+        t_first = t0 = __builtin_amdgcn_s_memrealtime();
+        if (cross && leader) atomicAdd(st + AME_ST_CROSS, 1u);
+    }
+    __device__ __forceinline__ int poll() {
+        if (ame_st_load(st, 0) != 0u) {
+            if (leader) atomicAdd(st + AME_ST_QUIET, 1u);
+            return 1;
+        }
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (!cross && ame_st_load(st, AME_ST_CROSS) != 0u) {
+            t0 = now;
+            return 0;
+        }
+        return (now - t0 > (cross ? AME_SPIN_TICKS_HALO : AME_SPIN_TICKS_LOCAL)) ? 2 : 0;
+    }
+    __device__ __forceinline__ uint64_t waited() const { return __builtin_amdgcn_s_memrealtime() - t_first; }
+    __device__ __forceinline__ void end() {
+        if (cross && leader) {
+            atomicSub(st + AME_ST_CROSS, 1u);
+            if (acct > 0) atomicAdd(st + acct, (uint32_t)(waited() / 100u));
+        }
+    }
+};
+
 // Constant part of the precision at global time tg (structured_mf.py:251-264):
 //   [t==0] Sigma0^-1 + [t>0] Q^-1 + [t<T-1] Phi^T Q^-1 Phi.
 __device__ __forceinline__ double pconst_entry(const double* consts, int D, int k, int m, int tg,
@@ -173,9 +251,13 @@ __host__ __device__ inline uint32_t ame_gw_tag(uint32_t epoch, int m) {
 __host__ __device__ inline long long ame_v2_worker_lds(int n, int R, int mode = 2) {
     const int nw = ame_v2_nworkers(mode);
     const int NW = (n + nw - 1) / nw, ZN = 4 * ame_v2_maxpw(mode);
-    // zb, red, and (MODES 3, 4) the LDS-held node slots [4 waves][MAXPW - NREG][64]
+    // zb, red, (MODES 3, 4) the LDS-held node slots [4 waves][MAXPW - NREG][64],
+    // and 16 bytes for the worker's dead word (ame_v2_worker_dead_off)
     const long long mld = 4LL * 4 * (ame_v2_maxpw(mode) - ame_v2_nreg(mode)) * 64;
-    return ame_align16(8LL * (NW > ZN ? NW : ZN)) + ame_align16(4LL * 4 * (2 * R + 2)) + mld;
+    return ame_align16(8LL * (NW > ZN ? NW : ZN)) + ame_align16(4LL * 4 * (2 * R + 2)) + mld + 16;
+}
+__host__ __device__ inline long long ame_v2_worker_dead_off(int n, int R, int mode) {
+    return ame_v2_worker_lds(n, R, mode) - 16;
 }
 __host__ __device__ inline long long ame_v2_mode_lds(int n, int R, int mode) {
     const long long m = sweep_lds_layout(n, R, mode != 0 ? 1 : 0, mode >= 2 ? 1 : 0).total;

@@ -52,7 +52,35 @@ __global__ void selftest_kernel(const float* src, float* out) {
     out[768 + lane] = l2[lane];
 }
 
+// CU hog (tests/test_gpu_coresidency.py): each workgroup holds `lds` bytes of
+// LDS, so no sweep workgroup fits beside it on its CU, and sleeps until
+// `ticks` of the 100 MHz clock have passed since it started; then it exits.
+// Every wave reaches the exit on its own clock: the grid always drains.
+__global__ void occupy_kernel(unsigned long long ticks, int* touched) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) smem[0] = 1;
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(64);
+    if (threadIdx.x == 0 && blockIdx.x == 0) *touched = (int)smem[0];
+}
+
 }  // namespace
+
+// Diagnostic: `workgroups` one-wave workgroups of `lds_bytes` LDS each that stay
+// resident for `microseconds` (at most 5 s), on `stream`.  Not part of
+// include/ame_amd.h.
+extern "C" int ame_debug_occupy(int workgroups, int lds_bytes, unsigned int microseconds, int* touched,
+                                void* stream) {
+    if (workgroups < 1 || workgroups > 4096 || lds_bytes < 0 || lds_bytes > 160 * 1024 ||
+        microseconds > 5000000u || touched == nullptr)
+        return -1;
+    if (hipFuncSetAttribute((const void*)occupy_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes) !=
+        hipSuccess)
+        return -2;
+    hipLaunchKernelGGL(occupy_kernel, dim3(workgroups), dim3(64), (size_t)lds_bytes, (hipStream_t)stream,
+                       100ull * microseconds, touched);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
 
 extern "C" int ame_debug_selftest(const float* src_dev, float* out_dev) {
     hipLaunchKernelGGL(selftest_kernel, dim3(1), dim3(64), 8192, 0, src_dev, out_dev);

@@ -261,48 +261,13 @@ __device__ __forceinline__ void set_slot(float (&mreg)[N], int sn, float val, bo
 // follows, AME_SWEEP_FLAG_NEXT_GROUP), or for the rank's last slice the right
 // rank's back-channel done word.  Same epoch window as ame_sweep3.hip: a flag
 // above wait_epoch cannot be current and sets AME_STATUS_STALE_EPOCH.
-__device__ __forceinline__ void ame_v2_wait_prev(const ame_sweep_args& a, int t, int TL, bool back_rd,
-                                                 int nd /* n * d: the back channel's done word */) {
+// Thread 0 waits (ame_wait_prev_done: the wait rules of include/ame_amd.h);
+// `dead` is set on thread 0 when it failed or gave up.
+__device__ __forceinline__ void ame_v2_wait_prev(const ame_sweep_args& a, int t, int TL, int tg, bool back_rd,
+                                                 int nd /* n * d: the back channel's done word */,
+                                                 bool& dead, bool account) {
     if (a.wait_epoch == 0u) return;
-    if (threadIdx.x == 0) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        const int qn = (t + 1 < TL || (a.flags & AME_SWEEP_FLAG_NEXT_GROUP)) ? 2 : 1;
-        for (int q = 0; q < qn; ++q) {
-            while (true) {
-                const uint32_t dv = __hip_atomic_load(a.done + t + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (dv > a.wait_epoch) {
-                    atomicOr(a.status, AME_STATUS_STALE_EPOCH);
-                    break;
-                }
-                if (dv == a.wait_epoch) break;
-                if (__builtin_amdgcn_s_memrealtime() - t0 > AME_SPIN_TICKS_LOCAL) {
-                    atomicOr(a.status, AME_STATUS_SPIN_TIMEOUT);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(8);
-            }
-        }
-        if (back_rd) {   // the right rank's first slice of the previous sweep
-            const uint32_t* bd = (const uint32_t*)(a.back_in + AME_BACK_DONE_OFFSET(nd));
-            while (true) {
-                const uint32_t dv = __hip_atomic_load(const_cast<uint32_t*>(bd), __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_SYSTEM);
-                if (dv > a.wait_epoch) {
-                    atomicOr(a.status, AME_STATUS_STALE_EPOCH);
-                    break;
-                }
-                if (dv == a.wait_epoch) break;
-                if (__builtin_amdgcn_s_memrealtime() - t0 > AME_SPIN_TICKS_HALO) {
-                    atomicOr(a.status, AME_STATUS_HALO_TIMEOUT);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(8);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (threadIdx.x == 0) ame::ame_wait_prev_done(a, t, TL, tg, back_rd, nd, dead, account);
     __syncthreads();
 }
 
@@ -339,11 +304,19 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
     const float r00f = (float)a.rinv[0], r01f = (float)a.rinv[1], r10f = (float)a.rinv[2], r11f = (float)a.rinv[3];
     const bool col = lane < M2;
     bool dead = false;
+    // set by a wave whose wait failed or gave up: the worker then tags its
+    // partials 0, which no slice waits for (include/ame_amd.h wait rules)
+    uint32_t* wdead = (uint32_t*)(smem + ame_v2_worker_dead_off(n, R, MODE));
+    if (tid == 0) *wdead = 0u;
+    __syncthreads();
     // MODE 3, pipelined launch: this worker's inputs (old means of slices t and
     // t+1) are the previous sweep's outputs -- wait for its done flags as the
     // slice's workgroup does (ame_v2_wait_prev)
     const bool back_rd = (MODE == 3) && (a.wait_epoch != 0u) && (t == TL - 1) && (a.back_in != nullptr);
-    if constexpr (MODE == 3) ame_v2_wait_prev(a, t, TL, back_rd, n * D);
+    if constexpr (MODE == 3) {
+        ame_v2_wait_prev(a, t, TL, dm.t_begin + t, back_rd, n * D, dead, false);   // the slice accounts
+        if (tid == 0 && dead) *wdead = 1u;
+    }
     // Right-neighbour AR terms PhiTQi mu_{j,t+1}^old of this worker's nodes, for
     // the slice workgroup's phase 2 (same products, order and zero padding as
     // its in-sweep form): formed here, before partial 0, and released with it --
@@ -437,7 +410,7 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
                 ok = (uint32_t)(v >> 32) == a.epoch;
             }
             if (!__all(ok) && !dead) {
-                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                AmeSpin w(a.status, false, lane == 0);
                 while (true) {
                     __builtin_amdgcn_s_sleep(2);
                     bool stale = false;
@@ -446,23 +419,28 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
                         ok = (uint32_t)(v >> 32) == a.epoch;
                         stale = (uint32_t)(v >> 32) > a.epoch;   // no later sweep can have written it yet
                     }
-                    if (__any(stale)) {
-                        if (lane == 0) atomicOr(a.status, AME_STATUS_STALE_EPOCH);
-                        dead = true;
-                        break;
-                    }
-                    if (__all(ok)) break;
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > AME_SPIN_TICKS_LOCAL) {
-                        if (lane == 0) atomicOr(a.status, AME_STATUS_SPIN_TIMEOUT);
+                    const bool st_hit = __any(stale);
+                    if (__all(ok) && !st_hit) break;
+                    const int r = st_hit ? 3 : w.poll();
+                    if (r != 0) {
+                        const uint64_t bad = __ballot(!ok);
+                        const int fl = bad ? (int)__builtin_ctzll(bad) : 0;
+                        const uint32_t obs = (uint32_t)(__shfl(v, fl) >> 32);
+                        if (lane == 0 && r >= 2)
+                            ame_fail(a.status, r == 3 ? AME_STATUS_STALE_EPOCH : AME_STATUS_SPIN_TIMEOUT,
+                                     AME_WAIT_WORKER_GRAN, dm.t_begin + t, (uint32_t)jn, obs, a.epoch, w.waited(),
+                                     a.epoch);
 #ifdef AME_WDEBUG
                         if (lane == 0)
                             printf("worker t=%d g=%d m=%d jn=%d q=%d: granule epoch %u want %u\n", t, g, m, jn,
-                                   q, (uint32_t)(v >> 32), a.epoch);
+                                   q, obs, a.epoch);
 #endif
+                        if (lane == 0) *wdead = 1u;
                         dead = true;
                         break;
                     }
                 }
+                w.end();
             }
             const float val = __uint_as_float((uint32_t)v);
             const int snu = __builtin_amdgcn_readfirstlane(sn);   // wave-uniform (owner wave)
@@ -534,7 +512,7 @@ __device__ __forceinline__ void gemv_worker(const ame_dims& dm, const ame_sweep_
         lds_barrier();
         if (tid < PW) {
             const float v = ((red[tid] + red[PW + tid]) + red[2 * PW + tid]) + red[3 * PW + tid];
-            const uint32_t tag = ame_gw_tag(a.epoch, m);
+            const uint32_t tag = (*wdead != 0u) ? 0u : ame_gw_tag(a.epoch, m);
             gran_store_agent(hp + (size_t)(m % AME_GW_RING) * PW + tid,
                              ((uint64_t)tag << 32) | (uint64_t)__float_as_uint(v));
         }
@@ -694,9 +672,13 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         else return M + j * M2;
     };
 
+    // set by a wave whose wait failed or gave up; wave 0 then tags its hand-off
+    // granules 0 and the slice flags nothing (include/ame_amd.h wait rules)
+    uint32_t* wdead = (uint32_t*)(scal + 62);
     // pipelined launch (MODE 3): the previous sweep's slices t, t+1 first
     if constexpr (PIPE)
-        ame_v2_wait_prev(a, tl, TL, (a.wait_epoch != 0u) && (tl == TL - 1) && (a.back_in != nullptr), n * D);
+        ame_v2_wait_prev(a, tl, TL, tg, (a.wait_epoch != 0u) && (tl == TL - 1) && (a.back_in != nullptr), n * D,
+                         dead, true);
 
     // ------------------------------------------------------------------
     // init: slice state, P_0 = P_const + sum_{j != 0} F_j, K_0 = P_0^-1
@@ -709,7 +691,10 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         }
     }
     if (tid < D) pcd[tid] = pconst_entry(a.consts, D, tid, tid, tg, Tt);
-    if (tid == 0) wsync[0] = wsync[1] = 0u;
+    if (tid == 0) {
+        wsync[0] = wsync[1] = 0u;
+        *wdead = dead ? 1u : 0u;   // thread 0 ran the pipelined wait
+    }
     __syncthreads();
     // entry (k, m) of P_0 from its node sum (k >= 2: sum of U/V entries, or of
     // products of two); k < 2 rows are constants times n - 1
@@ -1048,27 +1033,36 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
 #pragma unroll
         for (int u = 0; u < GE; ++u) ok = ok && (!((gvalid >> u) & 1u) || (uint32_t)(v[u] >> 32) == want);
         if (!ok && !dead) {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            // per thread (each holds its own partial words); every thread that
+            // gives up reports (ame_fail keeps the first record)
+            AmeSpin w(a.status, false, true);
             while (true) {
                 __builtin_amdgcn_s_sleep(1);
                 ok = true;
+                uint32_t obs = want;
 #pragma unroll
                 for (int u = 0; u < GE; ++u) {
                     if (((gvalid >> u) & 1u) && (uint32_t)(v[u] >> 32) != want) {
                         v[u] = gran_load_agent(hs + goff[u]);
                         ok = ok && (uint32_t)(v[u] >> 32) == want;
+                        if ((uint32_t)(v[u] >> 32) != want) obs = (uint32_t)(v[u] >> 32);
                     }
                 }
                 if (ok) break;
-                if (__builtin_amdgcn_s_memrealtime() - t0 > AME_SPIN_TICKS_LOCAL) {
-                    atomicOr(a.status, AME_STATUS_SPIN_TIMEOUT);
+                const int r = w.poll();
+                if (r != 0) {
+                    if (r == 2)
+                        ame_fail(a.status, AME_STATUS_SPIN_TIMEOUT, AME_WAIT_PARTIAL, tg, (uint32_t)node, obs, want,
+                                 w.waited(), a.epoch);
 #ifdef AME_WDEBUG
                     printf("main tl=%d node=%d: partial tags stale (want %x)\n", tl, node, want);
 #endif
+                    *wdead = 1u;
                     dead = true;
                     break;
                 }
             }
+            w.end();
         }
 #pragma unroll
         for (int u = 0; u < GE; ++u) {
@@ -1169,12 +1163,12 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             if (lane + 64 * h < D) ok = ok && (uint32_t)(v[h] >> 32) == a.epoch;
         }
         if (!__all(ok) && !dead) {
-            const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-            const uint64_t budget = from_halo ? AME_SPIN_TICKS_HALO : AME_SPIN_TICKS_LOCAL;
+            AmeSpin w(a.status, from_halo, lane == 0, AME_ST_HALO_US);
             while (true) {
                 __builtin_amdgcn_s_sleep(2);
                 ok = true;
                 bool stale = false;
+                uint32_t obs = a.epoch;
 #pragma unroll
                 for (int h = 0; h < KH; ++h) {
                     const int k = lane + 64 * h;
@@ -1182,22 +1176,27 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                         v[h] = from_halo ? gran_load_system(src + k) : gran_load_agent(src + k);
                         ok = ok && (uint32_t)(v[h] >> 32) == a.epoch;
                         stale = stale || (uint32_t)(v[h] >> 32) > a.epoch;   // see ame_sweep3.hip gran_finish
+                        if ((uint32_t)(v[h] >> 32) != a.epoch) obs = (uint32_t)(v[h] >> 32);
                     }
                 }
-                if (__any(stale)) {
-                    if (lane == 0) atomicOr(a.status, AME_STATUS_STALE_EPOCH);
-                    dead = true;
-                    break;
-                }
-                if (__all(ok)) break;
-                if (__builtin_amdgcn_s_memrealtime() - t_start > budget) {
-                    if (lane == 0)
-                        atomicOr(a.status, from_halo ? AME_STATUS_HALO_TIMEOUT
-                                                     : AME_STATUS_SPIN_TIMEOUT);
+                const bool st_hit = __any(stale);
+                if (__all(ok) && !st_hit) break;
+                const int r = st_hit ? 3 : w.poll();
+                if (r != 0) {
+                    const uint64_t bad = __ballot(!ok);
+                    const uint32_t o1 = __shfl(obs, bad ? (int)__builtin_ctzll(bad) : 0);
+                    if (lane == 0 && r >= 2)
+                        ame_fail(a.status,
+                                 r == 3 ? AME_STATUS_STALE_EPOCH
+                                        : (from_halo ? AME_STATUS_HALO_TIMEOUT : AME_STATUS_SPIN_TIMEOUT),
+                                 from_halo ? AME_WAIT_GRAN_HALO : AME_WAIT_GRAN_LOCAL, tg, (uint32_t)node, o1,
+                                 a.epoch, w.waited(), a.epoch);
+                    if (lane == 0) *wdead = 1u;
                     dead = true;
                     break;
                 }
             }
+            w.end();
         }
 #pragma unroll
         for (int h = 0; h < KH; ++h)
@@ -1596,6 +1595,9 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
         STAMP(1);
         // ---------------- phase 2 ----------------
         if (wave == 0) {
+            // any wave of the slice dead (its word was written before B1 or an
+            // earlier barrier): read with the step's first LDS reads
+            const bool wd = dead || *wdead != 0u;
             // lane owns state rows k = lane + 64h (h < KH)
             double W0[KH], W1[KH], Y0[KH], Y1[KH], ua[KH], uM[KH], gk[KH], K0[KH], K1[KH];
             double jp0[KH], jp1[KH], jn0[KH], jn1[KH];
@@ -1706,7 +1708,8 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                     mu_prev[k] = nw;
                     if constexpr (WK) mu_prev64[k] = (double)nw;
                     if constexpr (WK) mring[(i & 3) * D + k] = nw;
-                    const uint64_t g = ((uint64_t)a.epoch << 32) | (uint64_t)__float_as_uint(nw);
+                    // a dead slice tags its granules 0: no sweep waits for that epoch
+                    const uint64_t g = ((uint64_t)(wd ? 0u : a.epoch) << 32) | (uint64_t)__float_as_uint(nw);
                     gran_store_agent(a.hand + ((size_t)tl * n + i) * D + k, g);
                     if (tl == TL - 1 && a.halo_out != nullptr)
                         gran_store_system(a.halo_out + (size_t)i * D + k, g);
@@ -1810,12 +1813,13 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                 // soon as its input is in LDS
                 P2STAMP(2 * (wave - 1));
                 if (lane == 0) ame::lds_signal_add(wave == 1 ? wsync + 1 : wsync, 1u);
-                ame::lds_wait_ge(wsync + 1, (uint32_t)(i + 1), a.status, dead);
+                ame::lds_wait_ge(wsync + 1, (uint32_t)(i + 1), a.status, dead, tg, (uint32_t)i, a.epoch);
                 P2STAMP(8 + 2 * (wave - 1));
                 ar_left_finish(i + 1, aR);
                 P2STAMP(9 + 2 * (wave - 1));
                 P2STAMP(6);
-                ame::lds_wait_ge(wsync, 2u * (uint32_t)(i + 1), a.status, dead);
+                ame::lds_wait_ge(wsync, 2u * (uint32_t)(i + 1), a.status, dead, tg, (uint32_t)i, a.epoch);
+                if (dead && lane == 0) *wdead = 1u;
                 gemv_reduce(i + 1);
                 STAMPW(26, 64);
                 STAMPW(27, 128);
@@ -1955,19 +1959,24 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     cov_flush(n - 1);
     // ---- slice done: release its means, covariances and granules, then flag it
     // for the next sweep (ame_sweep3.hip's epilogue; every wave drains its own
-    // stores first) ----
+    // stores first).  A dead slice flags nothing ----
+    bool any_dead = false;
     if (a.done != nullptr || (tl == 0 && a.back_out != nullptr)) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // (the LDS word, not __syncthreads_or: that one adds 256 bytes of
+        // static LDS to the launch)
+        if (dead) *wdead = 1u;
         __syncthreads();
+        any_dead = *wdead != 0u;
     }
-    if (a.done != nullptr && tid == 0) {
+    if (a.done != nullptr && tid == 0 && !any_dead) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_store(a.done + tl, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // ---- first slice of a rank with a left neighbour: its new means are that
     // rank's next_old in the next (pipelined) sweep; system-scope release ----
-    if (tl == 0 && a.back_out != nullptr) {
+    if (tl == 0 && a.back_out != nullptr && !any_dead) {
         for (int e = tid; e < n * D; e += AME_NT)
             a.back_out[e] = __uint_as_float(__hip_atomic_load(
                 const_cast<uint32_t*>((const uint32_t*)(xn + e)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));

@@ -254,7 +254,10 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     auto gran_src = [&](int node) -> const uint64_t* {
         return (tl == 0) ? a.halo_in + (size_t)node * D : a.hand + ((size_t)(tl - 1) * n + node) * D;
     };
-    // v = granule of this lane (k = lane < D) as read earlier; spin until its tag is current
+    // v = granule of this lane (k = lane < D) as read earlier; spin until its tag
+    // is current.  A failed wait (AmeSpin rules, include/ame_amd.h) marks this
+    // wave dead and passes AME_LDS_DEAD to the solver through gcnt, so the slice
+    // stops publishing current-epoch granules and its done flag.
     auto gran_finish = [&](int node, uint64_t v, float* dst) {
         if (tg == 0) {
             if (lane < D) dst[lane] = 0.f;
@@ -262,8 +265,8 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         }
         bool ok = (lane >= D) || (uint32_t)(v >> 32) == a.epoch;
         if (!__all(ok) && !dead) {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            const uint64_t budget = (tl == 0) ? AME_SPIN_TICKS_HALO : AME_SPIN_TICKS_LOCAL;
+            const bool cross = tl == 0;
+            AmeSpin w(a.status, cross, lane == 0, hw == 0 ? AME_ST_HALO_US : 0);   // hw 0-2 wait alike
             const uint64_t* src = gran_src(node);
             while (true) {
                 // a tag above this sweep's epoch cannot come from slice t-1 of
@@ -271,24 +274,31 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 // for this slice's done flag): stale memory, reported, not consumed
                 bool stale = false;
                 if (lane < D) {
-                    v = (tl == 0) ? gran_load_system(src + lane) : gran_load_agent(src + lane);
+                    v = cross ? gran_load_system(src + lane) : gran_load_agent(src + lane);
                     ok = (uint32_t)(v >> 32) == a.epoch;
                     stale = (uint32_t)(v >> 32) > a.epoch;
                 }
-                if (__any(stale)) {
-                    if (lane == 0) atomicOr(a.status, AME_STATUS_STALE_EPOCH);
-                    dead = true;
-                    break;
-                }
-                if (__all(ok)) break;
-                if (__builtin_amdgcn_s_memrealtime() - t0 > budget) {
+                const bool st_hit = __any(stale);
+                if (__all(ok) && !st_hit) break;
+                const int r = st_hit ? 3 : w.poll();
+                if (r != 0) {
+                    // the record names the first lane whose tag is not current
+                    const uint64_t bad = __ballot(!ok);
+                    const int fl = bad ? (int)__builtin_ctzll(bad) : 0;
+                    const uint32_t obs = (uint32_t)(__shfl(v, fl) >> 32);
+                    if (lane == 0 && r >= 2)
+                        ame_fail(a.status, (r == 3) ? AME_STATUS_STALE_EPOCH
+                                                    : (cross ? AME_STATUS_HALO_TIMEOUT : AME_STATUS_SPIN_TIMEOUT),
+                                 cross ? AME_WAIT_GRAN_HALO : AME_WAIT_GRAN_LOCAL, tg, (uint32_t)node, obs,
+                                 a.epoch, w.waited(), a.epoch);
                     if (lane == 0)
-                        atomicOr(a.status, (tl == 0) ? AME_STATUS_HALO_TIMEOUT : AME_STATUS_SPIN_TIMEOUT);
+                        __hip_atomic_fetch_or(gcnt, AME_LDS_DEAD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     dead = true;
                     break;
                 }
                 __builtin_amdgcn_s_sleep(2);
             }
+            w.end();
         }
         if (lane < D) dst[lane] = __uint_as_float((uint32_t)v);
     };
@@ -348,55 +358,18 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     // (their means and covariances are this sweep's inputs; slice t+1 also reads
     // this slice's hand-off granules, which this sweep overwrites)
     if (a.wait_epoch != 0u) {
-        if (tid == 0) {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            // Epoch window: while this sweep (wait_epoch + 1) waits, neither flag
-            // can exceed wait_epoch -- sweep wait_epoch + 1 writes done[t] only
-            // when it finishes slice t, the sweeps queued behind it wait for that,
-            // and slice t+1 cannot finish before slice t.  A larger value is stale
-            // memory (a recycled buffer, a host write not yet ordered before this
-            // launch): it sets AME_STATUS_STALE_EPOCH instead of being taken as done.
-            // (done[TL]: the next slice group's first slice, when one follows)
-            const int qn = (tl + 1 < TL || (a.flags & AME_SWEEP_FLAG_NEXT_GROUP)) ? 2 : 1;
-            for (int q = 0; q < qn; ++q) {
-                while (true) {
-                    const uint32_t dv = __hip_atomic_load(a.done + tl + q, __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT);
-                    if (dv > a.wait_epoch) {
-                        atomicOr(a.status, AME_STATUS_STALE_EPOCH);
-                        break;
-                    }
-                    if (dv == a.wait_epoch) break;
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > AME_SPIN_TICKS_LOCAL) {
-                        atomicOr(a.status, AME_STATUS_SPIN_TIMEOUT);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(8);
-                }
-            }
-            if (back_rd) {   // the right rank's first slice of the previous sweep
-                const uint32_t* bd = (const uint32_t*)(a.back_in + AME_BACK_DONE_OFFSET(n * D));
-                while (true) {
-                    // same window: the right rank's first slice of THIS sweep
-                    // needs this slice's hand-off granules before it can finish
-                    const uint32_t dv = __hip_atomic_load(const_cast<uint32_t*>(bd), __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_SYSTEM);
-                    if (dv > a.wait_epoch) {
-                        atomicOr(a.status, AME_STATUS_STALE_EPOCH);
-                        break;
-                    }
-                    if (dv == a.wait_epoch) break;
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > AME_SPIN_TICKS_HALO) {
-                        atomicOr(a.status, AME_STATUS_HALO_TIMEOUT);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(8);
-                }
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+        // Epoch window: while this sweep (wait_epoch + 1) waits, neither flag can
+        // exceed wait_epoch -- sweep wait_epoch + 1 writes done[t] only when it
+        // finishes slice t, the sweeps queued behind it wait for that, and slice
+        // t+1 cannot finish before slice t.  A larger value is stale memory (a
+        // recycled buffer, a host write not yet ordered before this launch): it
+        // sets AME_STATUS_STALE_EPOCH instead of being taken as done.  (done[TL]:
+        // the next slice group's first slice, when one follows.)  The back
+        // channel (the right rank's first slice of the previous sweep) has the
+        // same window: that slice of THIS sweep needs this slice's granules.
+        // tid 0 waits; a failure marks it dead, which the solver wave (tid 0 is
+        // its lane 0) takes over, so the slice publishes nothing current.
+        if (tid == 0) ame_wait_prev_done(a, tl, TL, tg, back_rd, n * D, dead);
         __syncthreads();
     }
     // P_0 = Pconst + sum_{j>=1} F_j(old), F_j = J_j^T R^-1 J_j (fp64), and its
@@ -706,6 +679,9 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     if (wave == 0) {
         // ============================ SOLVER ============================
         __builtin_amdgcn_s_setprio(3);
+        // the prologue's wait ran on lane 0; node 0's hand-off wait (hw 0-2) leaves
+        // AME_LDS_DEAD in gcnt
+        dead = __any(dead) || (*(volatile uint32_t*)gcnt & AME_LDS_DEAD) != 0u;
         const int k = lane;
         const bool kl = k < D;
         const int kc = kl ? k : 0;
@@ -887,7 +863,12 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
 #endif
                 nw = mul_add_rn(lr, (float)mus, om, mold);
                 xn[(size_t)i * D + k] = nw;
+                // a dead slice tags its granules 0: no sweep waits for that epoch
+#ifdef AME_R6_NO_TAGGATE
                 const uint64_t gr = ((uint64_t)a.epoch << 32) | (uint64_t)__float_as_uint(nw);
+#else
+                const uint64_t gr = ((uint64_t)(dead ? 0u : a.epoch) << 32) | (uint64_t)__float_as_uint(nw);
+#endif
                 gran_store_agent(a.hand + ((size_t)tl * n + i) * D + k, gr);
                 if (tl == TL - 1 && a.halo_out != nullptr)
                     gran_store_system(a.halo_out + (size_t)i * D + k, gr);
@@ -931,7 +912,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             Sip = Si;
             STAMP3(5);
             // next base rows, once every helper wave has written K_i
-            lds_wait_ge(kcnt, 7u * (uint32_t)(i + 1), a.status, dead);
+            lds_wait_ge(kcnt, 7u * (uint32_t)(i + 1), a.status, dead, tg, (uint32_t)i, a.epoch);
             STAMP3(6);
             const double* Kn = Kbuf + (size_t)ppar * KSZ;
             if (kl) {
@@ -940,7 +921,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             }
             STAMP3(7);
             if (i + 1 < n) {   // g_{i+1} and Jn of node i+2 from HF1 (hw 0..2)
-                lds_wait_ge(gcnt, 3u * (uint32_t)(i + 1), a.status, dead);
+                lds_wait_ge(gcnt, 3u * (uint32_t)(i + 1), a.status, dead, tg, (uint32_t)i, a.epoch);
                 STAMP3(8);
                 prep(i + 1);
                 STAMP3(9);
@@ -1089,10 +1070,19 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     // the last node's new covariance (staged by HB in the epilogue step n)
     if (wave == 5 && n >= 1) flush_cov(n - 1);
     // ---- slice done: release its means, covariances and granules, then flag it
-    // for the next sweep (every wave drains its own stores first) ----
-    if (a.done != nullptr) {
+    // for the next sweep (every wave drains its own stores first).  A slice with
+    // a failed or abandoned wait flags nothing: what waits on it gives up
+    // quietly (the status block already holds the cause) ----
+    bool any_dead = false;
+    if (a.done != nullptr || (tl == 0 && a.back_out != nullptr)) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // (an LDS word, not __syncthreads_or: that one adds 256 bytes of static
+        // LDS to the launch)
+        if (dead) flags[1] = 1u;
         __syncthreads();
+        any_dead = flags[1] != 0u;
+    }
+    if (a.done != nullptr && !any_dead) {
         if (tid == 0) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1101,7 +1091,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     }
     // ---- first slice of a rank with a left neighbour: its new means are that
     // rank's next_old in the next (pipelined) sweep; system-scope release ----
-    if (tl == 0 && a.back_out != nullptr) {
+    if (tl == 0 && a.back_out != nullptr && !any_dead) {
         for (int e = tid; e < n * D; e += kNT)
             a.back_out[e] = __uint_as_float(__hip_atomic_load(
                 const_cast<uint32_t*>((const uint32_t*)(xn + e)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));

@@ -27,12 +27,41 @@ __device__ __forceinline__ void lds_signal_set(uint32_t* f, uint32_t v) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// Bounded: a wait that outlives AME_SPIN_TICKS_LOCAL sets AME_STATUS_LDS_TIMEOUT
-// and gives up (the launch then finishes with wrong values, never hangs).
-__device__ __forceinline__ void lds_wait_ge(uint32_t* f, uint32_t target, uint32_t* status, bool& dead) {
-    if (!dead && __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
+// A wave whose global wait failed adds this bit to the LDS counter it signals
+// next, so the wave waiting on that counter (the one that publishes the slice's
+// hand-off granules) learns it without an extra LDS read (AME_STATUS_WORDS).
+#define AME_LDS_DEAD 0x40000000u
+// The slow path of lds_wait_ge (AmeSpin rules), out of line: inlined, its
+// record stores cost the v3 solver loop VGPR spills.  Returns the counter's
+// value, with AME_LDS_DEAD set when the wait failed or gave up (one wave).
+static __device__ __attribute__((noinline)) uint32_t lds_wait_slow(uint32_t* f, uint32_t target, uint32_t* status,
+                                                                   int slice, uint32_t node, uint32_t epoch) {
+    const bool ld = (threadIdx.x & 63) == 0;
+    AmeSpin w(status, false, ld);
+    uint32_t v;
+    while ((v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        const int r = w.poll();
+        if (r == 0) continue;
+        if (r == 2 && ld)
+            ame_fail(status, AME_STATUS_LDS_TIMEOUT, AME_WAIT_LDS, slice, node, v, target, w.waited(), epoch);
+        v |= AME_LDS_DEAD;
+        break;
+    }
+    w.end();
+    return v;
+}
+// Bounded: a wait that outlives its budget sets AME_STATUS_LDS_TIMEOUT and gives
+// up (the launch then finishes with wrong values and a raised status, never
+// hangs).  A counter carrying AME_LDS_DEAD marks the waiting wave dead as well.
+__device__ __forceinline__ void lds_wait_ge(uint32_t* f, uint32_t target, uint32_t* status, bool& dead,
+                                            int slice = 0, uint32_t node = AME_NODE_NONE,
+                                            uint32_t epoch = 0) {
+    uint32_t v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef AME_R6_LDS_SIMPLE
+    if (!dead && v < target) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
+        while ((v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < target) {
             __builtin_amdgcn_s_sleep(1);
             if (__builtin_amdgcn_s_memrealtime() - t0 > AME_SPIN_TICKS_LOCAL) {
                 if ((threadIdx.x & 63) == 0) atomicOr(status, AME_STATUS_LDS_TIMEOUT);
@@ -41,7 +70,60 @@ __device__ __forceinline__ void lds_wait_ge(uint32_t* f, uint32_t target, uint32
             }
         }
     }
+#else
+    if (!dead && v < target) v = lds_wait_slow(f, target, status, slice, node, epoch);
+#endif
+    dead = dead || (v & AME_LDS_DEAD) != 0u;
     asm volatile("" ::: "memory");
+}
+
+// Pipelined launch (wait_epoch != 0), ONE thread: wait until the previous sweep
+// (epoch wait_epoch) flagged local slices t and t+1 done (done[t + 1] is the next
+// slice group's first slice under AME_SWEEP_FLAG_NEXT_GROUP) and, for a rank's
+// last slice, the right rank's back-channel done word.  A word above
+// wait_epoch is outside the protocol's window (AME_STATUS_STALE_EPOCH); the
+// back channel is a cross-rank wait (10 s budget, counted in the status
+// block), the done flags local ones (AmeSpin rules).  Any failure, or a quiet
+// give-up after another one, sets `dead` and skips the remaining waits.
+__device__ __forceinline__ void ame_wait_prev_done(const ame_sweep_args& a, int t, int TL, int tg,
+                                                   bool back_rd, int nd, bool& dead, bool account = true) {
+    const int qn = (t + 1 < TL || (a.flags & AME_SWEEP_FLAG_NEXT_GROUP)) ? 2 : 1;
+    for (int q = 0; q <= qn && !dead; ++q) {
+        const bool back = q == qn;
+        if (back && !back_rd) break;
+        const uint32_t* w = back ? (const uint32_t*)(a.back_in + AME_BACK_DONE_OFFSET(nd)) : a.done + t + q;
+        const int site = back ? AME_WAIT_BACK : (q == 0 ? AME_WAIT_DONE_SELF : AME_WAIT_DONE_RIGHT);
+        auto load = [&]() -> uint32_t {
+            return back ? __hip_atomic_load(const_cast<uint32_t*>(w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                        : __hip_atomic_load(const_cast<uint32_t*>(w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        };
+        uint32_t dv = load();
+        if (dv == a.wait_epoch) continue;
+        AmeSpin sp(a.status, back, true, (back && account) ? AME_ST_BACK_US : 0);
+        while (true) {
+            if (dv > a.wait_epoch) {
+                ame_fail(a.status, AME_STATUS_STALE_EPOCH, site, tg, AME_NODE_NONE, dv, a.wait_epoch,
+                         sp.waited(), a.epoch);
+                dead = true;
+                break;
+            }
+            if (dv == a.wait_epoch) break;
+            const int r = sp.poll();
+            if (r != 0) {
+                if (r == 2)
+                    ame_fail(a.status, back ? AME_STATUS_HALO_TIMEOUT : AME_STATUS_SPIN_TIMEOUT, site, tg,
+                             AME_NODE_NONE, dv, a.wait_epoch, sp.waited(), a.epoch);
+                dead = true;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(8);
+            dv = load();
+        }
+        sp.end();
+    }
+    if (back_rd) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // LDS-DMA: each lane's 16 (4) bytes from gsrc land at LDS byte lds + lane*16 (*4).

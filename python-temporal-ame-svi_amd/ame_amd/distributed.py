@@ -258,6 +258,29 @@ class TimeShardHalo:
         torch.cuda.synchronize(eng.dev)
 
     # ---- engine hooks ----
+    @staticmethod
+    def device_key(dev) -> tuple:
+        """Identity of a GPU across processes: host, PCI address and UUID."""
+        p = torch.cuda.get_device_properties(dev)
+        return (socket.gethostname(), int(getattr(p, "pci_domain_id", 0)),
+                int(getattr(p, "pci_bus_id", 0)), int(getattr(p, "pci_device_id", 0)),
+                str(getattr(p, "uuid", "")))
+
+    def device_sharers(self, eng) -> int:
+        """Number of ranks of the group that run on this rank's GPU (1 on a
+        node with one rank per GPU; k when k ranks share one, as the one-GPU
+        tests do).  The engine divides its co-resident slice budget by it: a
+        spinning launch of any of them may wait on a slice of another
+        (DESIGN.md §5).  Reference: none (single process)."""
+        if self.shard.world == 1:
+            return 1
+        if getattr(self, "_sharers", None) is None:
+            key = self.device_key(eng.dev)
+            keys = [None] * self.shard.world
+            dist.all_gather_object(keys, key, group=self.group)
+            self._sharers = sum(1 for k in keys if k == key)
+        return self._sharers
+
     def agree_max(self, eng, value: int) -> int:
         """The maximum of `value` over all ranks (the engines' epoch base)."""
         t = torch.tensor([int(value)], dtype=torch.int64,

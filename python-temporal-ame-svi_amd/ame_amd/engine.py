@@ -38,6 +38,7 @@ from __future__ import annotations
 import collections
 import ctypes
 import math
+import time
 from dataclasses import dataclass, fields
 from typing import Optional
 
@@ -170,6 +171,24 @@ def status_text(st: int) -> str:
     return "; ".join(parts) if parts else "unknown"
 
 
+def status_report(words) -> str:
+    """Text of a status block (include/ame_amd.h, AME_STATUS_WORDS uint32):
+    the bits, then the record of the FIRST failing wait (site, slice, node,
+    word seen vs expected, time waited, sweep epoch) and how many later waits
+    gave up quietly because of it."""
+    w = [int(x) & 0xFFFFFFFF for x in words]
+    w += [0] * (_lib.AME_STATUS_WORDS - len(w))
+    msg = f"device status {w[0]:#x}: {status_text(w[0])}"
+    if w[1]:
+        node = "prologue" if w[4] == 0xFFFFFFFF else f"node {w[4]}"
+        site = _lib.AME_WAIT_SITES.get(w[2], f"site {w[2]}")
+        msg += (f"; first failure: {site}, slice {w[3]}, {node}, saw {w[5]} expected {w[6]}, "
+                f"after {w[7] / 1e3:.1f} ms, sweep epoch {w[8]}")
+    if w[10]:
+        msg += f"; {w[10]} later wait(s) gave up quietly"
+    return msg
+
+
 def _ptr(t: Optional[torch.Tensor]):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
@@ -299,7 +318,8 @@ class DeviceEngine:
                 _lib.check(-1, "ame_elbo_work_size")
             self.work = torch.empty(ws, dtype=torch.float64, device=dev)
             self.out = torch.zeros(8, dtype=torch.float64, device=dev)
-            self.status = torch.zeros(1, dtype=torch.int32, device=dev)
+            self.status = torch.zeros(_lib.AME_STATUS_WORDS, dtype=torch.int32, device=dev)
+        self.last_status = None   # the status block of the last failure _check_status raised
         self.epoch = _epoch_base()
         if self.halo is not None:   # every rank's sweep k carries the same epoch
             self.epoch = self.halo.agree_max(self, self.epoch)
@@ -335,6 +355,17 @@ class DeviceEngine:
                 gd = _lib.ame_dims(self.n, self.r, w, sh.t_begin, sh.T_total, self.vcode)
                 if int(self.L.ame_sweep_kind(ctypes.byref(gd), req)) == _lib.AME_SWEEP_V2_WORKERS:
                     self.max_slices = w
+        # Ranks of one time-sharded run that share this GPU share its CUs, and a
+        # spinning launch of one rank can wait on a slice of another (halo, back
+        # channel): all of them must be co-resident at once, so each rank
+        # budgets for 1/k of the chip (co-residency rule)
+        self.device_sharers = self.halo.device_sharers(self) if self.halo is not None else 1
+        if self.device_sharers > 1:
+            self.max_slices //= self.device_sharers
+            if self.max_slices < 1:
+                raise RuntimeError(f"ame_amd: {self.device_sharers} ranks share this GPU and one "
+                                   f"sweep slice (n={self.n}, r={self.r}) does not fit 1/"
+                                   f"{self.device_sharers} of it")
         # Pipelined layout: a kernel that orders itself slice by slice on the
         # device (done flags) runs with TWO launches co-resident -- consecutive
         # sweeps, and consecutive slice groups of one sweep -- so each launch gets
@@ -384,13 +415,19 @@ class DeviceEngine:
         self._launch_ctr = 0
         self.done = torch.zeros(max(sh.T_local, 1), dtype=torch.int32, device=self.dev)
         kinds = set(self.group_kinds.values())
+        # slice workgroups of this kind the whole chip holds at once
+        self.resident_slots = int(self.L.ame_sweep_max_slices(self.n, self.r, self.sweep_kind))
         self.pipelined = (len(kinds) == 1 and pipe_cap > 0
                           and bool(self.L.ame_sweep_orders_slices(self.n, self.r, self.sweep_kind))
-                          and 2 * max(sz for _, sz in self.groups)
-                          <= int(self.L.ame_sweep_max_slices(self.n, self.r, self.sweep_kind))
+                          and 2 * max(sz for _, sz in self.groups) * self.device_sharers
+                          <= self.resident_slots
                           and bool(opt.pipeline))
         if self.halo is not None:   # every rank must take the same path
             self.pipelined = self.halo.agree(self, self.pipelined)
+        # launches of this process that may spin at once (pipelined: one per
+        # sweep stream); the co-residency rule is
+        #     device_sharers * coresident_launches * largest group <= resident_slots
+        self.coresident_launches = 2 if self.pipelined else 1
         # How many sweeps may run ahead of the committed state.  Pipelined sweeps
         # overlap slice by slice, so a deeper queue keeps the wavefront full when
         # its fill over all T slices (all ranks) exceeds one iteration: the host
@@ -425,6 +462,10 @@ class DeviceEngine:
         # launch skip the wait for host-issued writes, to show the device's
         # epoch-window check catching the resulting stale flags
         self._order_after_host_writes = True
+        # test hook only (tests/test_gpu_skew.py): seconds this rank sleeps before
+        # its first sweep launch, after that sweep's collectives -- a rank that
+        # arrives late, as host jitter or a slow first collective makes it
+        self._first_launch_delay_s = 0.0
         self._mark_host_writes()
 
     def _cu_stream(self, first, num, slot=0):
@@ -548,6 +589,9 @@ class DeviceEngine:
             next_old, halo_in, halo_out = self.halo.before_sweep(
                 self, gather=not pipe, first=self.xs[src][0])
             back_in, back_out = self.halo.back_channels(self)
+        if self._first_launch_delay_s:
+            time.sleep(self._first_launch_delay_s)
+            self._first_launch_delay_s = 0.0
         wait = self.epoch - 1 if pipe else 0
         ready = None
         if not pipe:
@@ -722,14 +766,14 @@ class DeviceEngine:
         return assemble(self.sums(speculate), self.n, self.T, self.d, self.variant, self.C)
 
     def _check_status(self):
-        st = int(self.status.item())
-        if st:
+        words = self.status.cpu().tolist()
+        if words[0]:
             self.status.zero_()
             # a later pipelined launch must not start before this zero lands (it
             # would erase that sweep's own status bits)
             self._mark_host_writes()
-            raise RuntimeError(f"ame_amd: sweep reported device status {st:#x}: "
-                               f"{status_text(st)}")
+            self.last_status = words
+            raise RuntimeError(f"ame_amd: sweep reported {status_report(words)}")
 
     def invalidate(self):
         self._out_valid = False

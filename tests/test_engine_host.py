@@ -47,3 +47,24 @@ def test_slice_groups_cover_in_order():
         assert max(sz for _, sz in g) <= (cap if force <= 0 else min(force, cap))
     with pytest.raises(RuntimeError):
         slice_groups(4, 0)
+
+
+def test_status_report_names_the_first_failure():
+    """The status block (include/ame_amd.h AME_STATUS_WORDS): bits, the first
+    failing wait's record, and the count of waits that gave up behind it."""
+    from ame_amd import _lib
+    from ame_amd.engine import status_report
+    assert _lib.AME_STATUS_WORDS == 16
+    w = [0] * 16
+    w[0] = _lib.AME_STATUS_SPIN_TIMEOUT
+    w[1], w[2], w[3], w[4], w[5], w[6], w[7], w[8] = 1, 4, 65, 17, 6, 7, 2_000_123, 7
+    w[10] = 12
+    msg = status_report(w)
+    assert msg.startswith("device status 0x1: a hand-off between slices timed out")
+    assert "first failure: hand-off granule of slice t-1, slice 65, node 17, saw 6 expected 7" in msg
+    assert "after 2000.1 ms, sweep epoch 7" in msg and "12 later wait(s) gave up quietly" in msg
+    w2 = [_lib.AME_STATUS_STALE_EPOCH, 1, 2, 3, 0xFFFFFFFF, 9, 4, 0, 5] + [0] * 7
+    assert "done flag of slice t+1 (previous sweep), slice 3, prologue, saw 9 expected 4" in status_report(w2)
+    # negative int32 words from the device tensor are read as uint32
+    w3 = [8, 1, 3, 0, -1, -2, 5, 0, 6] + [0] * 7
+    assert "prologue, saw 4294967294 expected 5" in status_report(w3)
