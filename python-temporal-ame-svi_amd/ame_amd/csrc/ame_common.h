@@ -55,25 +55,32 @@ __device__ __forceinline__ void ame_fail(uint32_t* st, uint32_t bit, int site, i
 // this GPU restarts its budget while any workgroup sharing the status block is
 // inside a cross-rank wait: its producer may stand behind that rank (no
 // progress is expected until it arrives, and that wait has its own budget).
+// The status words are read at most once per AME_SPIN_TICKS_CHECK: a poll
+// before that costs one clock read, as the plain bounded spin did (two global
+// loads per poll delayed every wake-up: +0.7 % at config 3,
+// profiles/r06_ab_prologue.txt).
 // acct (a cross-rank wait's leader only): status word that end() adds the
 // microseconds spent to -- AME_ST_HALO_US / AME_ST_BACK_US, the per-rank halo
 // wait time the bench reports; 0 = none.
+#define AME_SPIN_TICKS_CHECK (100ull * 1000)   // 1 ms
 struct AmeSpin {
     uint32_t* st;
-    uint64_t t_first, t0;
+    uint64_t t_first, t0, t_chk;
     bool cross, leader;
     int acct;
     __device__ __forceinline__ AmeSpin(uint32_t* s, bool cr, bool ld, int ac = 0)
         : st(s), cross(cr), leader(ld), acct(ac) {
-        t_first = t0 = __builtin_amdgcn_s_memrealtime();
+        t_first = t0 = t_chk = __builtin_amdgcn_s_memrealtime();
         if (cross && leader) atomicAdd(st + AME_ST_CROSS, 1u);
     }
     __device__ __forceinline__ int poll() {
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (now - t_chk < AME_SPIN_TICKS_CHECK) return 0;
+        t_chk = now;
         if (ame_st_load(st, 0) != 0u) {
             if (leader) atomicAdd(st + AME_ST_QUIET, 1u);
             return 1;
         }
-        const uint64_t now = __builtin_amdgcn_s_memrealtime();
         if (!cross && ame_st_load(st, AME_ST_CROSS) != 0u) {
             t0 = now;
             return 0;

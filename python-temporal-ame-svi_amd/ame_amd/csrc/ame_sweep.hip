@@ -716,83 +716,26 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     // the U/V column of row k (k >= 2) that J carries: row U_c has entry V_c, row V_c entry U_c
     auto jcol = [&](int k) { const int ck = k - 2; return ck < R ? R + ck : ck - R; };
     if constexpr (MG || WK) {
-        // The old (U,V) rows live in HBM here: staged through LDS in chunks of CH
-        // rows (cst is free until phase 3 of step 0).  Every entry keeps its own
-        // accumulator and adds the nodes in order, as the direct form below does
-        // (the same operations, the same roundings); the direct form made one
-        // dependent HBM / L2 round trip per node and entry -- at config 5's rank
-        // shape the prologue took ~2 200 node steps of the sweep
-        // (profiles/r05_c5_prologue_stamps.txt).
-        constexpr int CH = (D * D) / M2;
-        constexpr int NLQ = (NLT + AME_NT - 1) / AME_NT;
-        float* xs = cst;
-        // this thread's entries: the two U/V columns each reads (column 0 for an
-        // entry that takes no part) and the entry's kind; node-outer and
-        // branch-free below, so the entries' LDS reads batch and their fp64
-        // chains interleave -- each still adds its nodes in order with the
-        // direct form's operations (same roundings)
-        double acc[NLQ];
-        int ekc[NLQ], emc[NLQ];
-        bool live[NLQ], plain[NLQ];
-#pragma unroll
-        for (int qq = 0; qq < NLQ; ++qq) {
-            acc[qq] = 0.0;
-            ekc[qq] = emc[qq] = 0;
-            live[qq] = plain[qq] = false;
-            const int e = tid + AME_NT * qq;
-            if (e < NLT) {
-                int k, m;
-                tri_decode(e, k, m);
-                if (k >= 2) {
-                    live[qq] = true;
-                    ekc[qq] = jcol(k);
-                    plain[qq] = m < 2;
-                    emc[qq] = (m < 2) ? ekc[qq] : jcol(m);
-                }
-            }
+        // The old (U,V) rows live in HBM here.  Their Gram matrix, column sums
+        // and sums of squares on fp64 MFMA (p0_gram_mfma, ame_sweep_dev.h): the
+        // node-by-node loop before it made one dependent round trip per node,
+        // ~290 node steps of prologue per launch at config 5's rank shape
+        // (profiles/r05_c5_prologue_stamps.txt; 2 200 before round 5's staging).
+        // G lands in K's (U, V) block; red is free until the pivot loop.
+        double* colsum = red;
+        float* x0 = (float*)(red + M2);
+        ame::p0_gram_mfma<R, AME_NT / 64>(xo, n, D, K, KS, colsum, x0);
+        if (tid < M2) {   // node 0 joins the sums of squares
+            const int kq = 2 + (tid >= R ? tid - R : tid + R);   // the row that holds column tid
+            const double v = (double)x0[tid];
+            ssq[tid] = fma(v, v, K[kq * KS + kq]);
         }
-        const int sc = (tid < M2) ? tid : 0;
-        double sq = 0.0;
-        for (int j0 = 0; j0 < n; j0 += CH) {
-            const int nc = min(CH, n - j0);
-            __syncthreads();
-            for (int e = tid; e < nc * M2; e += AME_NT) {
-                const int jj = e / M2, c = e - jj * M2;
-                xs[e] = xo[(size_t)(j0 + jj) * D + 2 + c];
-            }
-            __syncthreads();
-            int js = 0;
-            if (j0 == 0) {   // node 0: in the sums of squares only
-                const double v = (double)xs[sc];
-                sq = fma(v, v, sq);
-                js = 1;
-            }
-            for (int jj = js; jj < nc; ++jj) {
-                const float* row = xs + jj * M2;
-                float xk[NLQ], xm[NLQ];
-                const float xs2 = row[sc];
-#pragma unroll
-                for (int qq = 0; qq < NLQ; ++qq) {
-                    xk[qq] = row[ekc[qq]];
-                    xm[qq] = row[emc[qq]];
-                }
-                sq = fma((double)xs2, (double)xs2, sq);
-#pragma unroll
-                for (int qq = 0; qq < NLQ; ++qq) {
-                    const double a_ = (double)xk[qq], b_ = (double)xm[qq];
-                    const double nv = plain[qq] ? acc[qq] + a_ : fma(a_, b_, acc[qq]);
-                    acc[qq] = live[qq] ? nv : acc[qq];
-                }
-            }
-        }
-        if (tid < M2) ssq[tid] = sq;
-#pragma unroll
-        for (int qq = 0; qq < NLQ; ++qq) {
-            const int e = tid + AME_NT * qq;
-            if (e >= NLT) continue;
+        __syncthreads();
+        for (int e = tid; e < NLT; e += AME_NT) {
             int k, m;
             tri_decode(e, k, m);
-            const double v = p0_entry(k, m, acc[qq]);
+            const double acc = (k < 2) ? 0.0 : (m < 2) ? colsum[jcol(k)] : K[k * KS + m];
+            const double v = p0_entry(k, m, acc);
             K[k * KS + m] = v;
             K[m * KS + k] = v;
         }

@@ -376,73 +376,34 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
     // inverse -> Kbuf[0] by the in-place symmetric sweep operator; naive variant:
     // column sums of squares of (U, V) over all nodes -> ssq[2 + c]
     {
-        constexpr int EQ = (NLT + kNT - 1) / kNT;
-        float* st = (float*)yring;   // staging: CH nodes x 2r (the rings are not live yet)
         double* piv = vbuf;
         double* K = Kbuf;
-        const int CH = min(64, (8 * YS) / M2);
         const double pp = r00, ss = r11, qq = 0.5 * (r01 + r10);
-        double acc[EQ];
-        int ek[EQ], em[EQ];
-#pragma unroll
-        for (int u = 0; u < EQ; ++u) {
-            acc[u] = 0.0;
-            const int e = tid + kNT * u;
-            int k = -1, m = -1;
-            if (e < NLT) tri_decode3(e, k, m);
-            ek[u] = k;
-            em[u] = m;
-        }
-        double sq = 0.0;
-        for (int j0 = 1; j0 < n; j0 += CH) {
-            const int cnt = min(CH, n - j0);
-            __syncthreads();
-            for (int e = tid; e < cnt * M2; e += kNT) {
-                const int jj = e / M2, c = e - jj * M2;
-                st[e] = xo[(size_t)(j0 + jj) * D + 2 + c];
-            }
-            __syncthreads();
-#pragma unroll
-            for (int u = 0; u < EQ; ++u) {
-                const int k = ek[u], m = em[u];
-                if (k < 2) continue;
-                const int ck = k - 2;
-                const int kc = (ck < R) ? R + ck : ck - R;   // row U_ck pairs with V, row V with U
-                double a0 = 0.0;
-                if (m < 2) {
-                    for (int jj = 0; jj < cnt; ++jj) a0 += (double)st[jj * M2 + kc];
-                } else {
-                    const int cm = m - 2;
-                    const int mc = (cm < R) ? R + cm : cm - R;
-                    for (int jj = 0; jj < cnt; ++jj)
-                        a0 = fma((double)st[jj * M2 + kc], (double)st[jj * M2 + mc], a0);
-                }
-                acc[u] += a0;
-            }
-            if (tid < M2)
-                for (int jj = 0; jj < cnt; ++jj) {
-                    const double v = (double)st[jj * M2 + tid];
-                    sq = fma(v, v, sq);
-                }
-        }
+        // G = sum_{j>=1} x_j x_j^T (fp64 MFMA, ame_sweep_dev.h) straight into K's
+        // (U, V) block, column sums into vbuf (free until the pivot loop)
+        double* colsum = vbuf;
+        float* x0 = (float*)(vbuf + M2);
+        p0_gram_mfma<R, kNT / 64>(xo, n, D, K, KS, colsum, x0);
         if (tid < M2) {   // node 0 joins the sums of squares
-            const double v = (double)xo[2 + tid];
-            ssq[2 + tid] = fma(v, v, sq);
+            const int kq = 2 + (tid >= R ? tid - R : tid + R);   // the row that holds column tid
+            const double v = (double)x0[tid];
+            ssq[2 + tid] = fma(v, v, K[kq * KS + kq]);
         }
-#pragma unroll
-        for (int u = 0; u < EQ; ++u) {
-            const int k = ek[u], m = em[u];
-            if (k < 0) continue;
+        __syncthreads();
+        for (int e = tid; e < NLT; e += kNT) {
+            int k, m;
+            tri_decode3(e, k, m);
             double v;
             if (k < 2) {
                 v = ((k == 0 && m == 0) ? pp : (k == 1 && m == 1) ? ss : qq) * (double)(n - 1);
             } else {
                 const bool ku = (k - 2) < R;
                 if (m < 2) {
-                    v = (ku ? (m == 0 ? pp : qq) : (m == 0 ? qq : ss)) * acc[u];
+                    const int ck = k - 2, kc = (ck < R) ? R + ck : ck - R;
+                    v = (ku ? (m == 0 ? pp : qq) : (m == 0 ? qq : ss)) * colsum[kc];
                 } else {
                     const bool mu_ = (m - 2) < R;
-                    v = ((ku && mu_) ? pp : ((!ku && !mu_) ? ss : qq)) * acc[u];
+                    v = ((ku && mu_) ? pp : ((!ku && !mu_) ? ss : qq)) * K[k * KS + m];
                 }
             }
             v += pconst_entry(a.consts, D, k, m, tg, Tt);
@@ -864,11 +825,7 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 nw = mul_add_rn(lr, (float)mus, om, mold);
                 xn[(size_t)i * D + k] = nw;
                 // a dead slice tags its granules 0: no sweep waits for that epoch
-#ifdef AME_R6_NO_TAGGATE
-                const uint64_t gr = ((uint64_t)a.epoch << 32) | (uint64_t)__float_as_uint(nw);
-#else
                 const uint64_t gr = ((uint64_t)(dead ? 0u : a.epoch) << 32) | (uint64_t)__float_as_uint(nw);
-#endif
                 gran_store_agent(a.hand + ((size_t)tl * n + i) * D + k, gr);
                 if (tl == TL - 1 && a.halo_out != nullptr)
                     gran_store_system(a.halo_out + (size_t)i * D + k, gr);

@@ -31,16 +31,23 @@ __device__ __forceinline__ void lds_signal_set(uint32_t* f, uint32_t v) {
 // next, so the wave waiting on that counter (the one that publishes the slice's
 // hand-off granules) learns it without an extra LDS read (AME_STATUS_WORDS).
 #define AME_LDS_DEAD 0x40000000u
-// The slow path of lds_wait_ge (AmeSpin rules), out of line: inlined, its
-// record stores cost the v3 solver loop VGPR spills.  Returns the counter's
-// value, with AME_LDS_DEAD set when the wait failed or gave up (one wave).
+// The spin of lds_wait_ge (AmeSpin rules), out of line.  Measured at config 3
+// (same box, 5 rounds, profiles/r06_ab_lds_wait.txt): out of line 2.424 ms per
+// iteration; the plain inline spin of rounds 1-5 2.542; the inline spin with
+// this call only after 1 ms 2.546; the rules inline (no call, 2 VGPR spills)
+// 2.441 -- the solver's loop schedules better without a spin loop inside it;
+// s_sleep 1 / 3 / 8 in this loop: 2.423 / 2.427 / 2.425 (r06_ab_sleep.txt).
+// (The helpers' granule wait out of line instead: 3.10 -- a call per wait on
+// hw 0-2, whose waits are frequent.)
+// Returns the counter's value, with AME_LDS_DEAD set when the wait failed or
+// gave up (one wave).
 static __device__ __attribute__((noinline)) uint32_t lds_wait_slow(uint32_t* f, uint32_t target, uint32_t* status,
                                                                    int slice, uint32_t node, uint32_t epoch) {
     const bool ld = (threadIdx.x & 63) == 0;
     AmeSpin w(status, false, ld);
     uint32_t v;
     while ((v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < target) {
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(8);
         const int r = w.poll();
         if (r == 0) continue;
         if (r == 2 && ld)
@@ -58,21 +65,7 @@ __device__ __forceinline__ void lds_wait_ge(uint32_t* f, uint32_t target, uint32
                                             int slice = 0, uint32_t node = AME_NODE_NONE,
                                             uint32_t epoch = 0) {
     uint32_t v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#ifdef AME_R6_LDS_SIMPLE
-    if (!dead && v < target) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while ((v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < target) {
-            __builtin_amdgcn_s_sleep(1);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > AME_SPIN_TICKS_LOCAL) {
-                if ((threadIdx.x & 63) == 0) atomicOr(status, AME_STATUS_LDS_TIMEOUT);
-                dead = true;
-                break;
-            }
-        }
-    }
-#else
     if (!dead && v < target) v = lds_wait_slow(f, target, status, slice, node, epoch);
-#endif
     dead = dead || (v & AME_LDS_DEAD) != 0u;
     asm volatile("" ::: "memory");
 }
@@ -124,6 +117,109 @@ __device__ __forceinline__ void ame_wait_prev_done(const ame_sweep_args& a, int 
     if (back_rd) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---- P_0's node sums on fp64 MFMA (sweep prologues, v3 and v2) ----
+// The base precision P_0 of a slice (structured_mf.py:251-264 summed over the
+// other nodes) needs, over the slice's old (U, V) rows x_j
+// (M2 = 2R floats, node 0 excluded): the Gram matrix G = sum_{j>=1} x_j x_j^T,
+// the column sums sum_{j>=1} x_j, and (naive) sum_{j>=0} x_j^2.  G is a
+// K = n - 1 GEMM: v_mfma_f64_16x16x4f64 over chunks of 4 nodes (lane l holds
+// x[4c + (l >> 4)][16 I + (l & 15)], the A operand of tile row I and the B
+// operand of tile column I alike; the accumulator of tile (I, J) holds row
+// 16 I + (l >> 4) + 4 v, column 16 J + (l & 15), as in ame_cov.hip), chunks
+// dealt round-robin to the NW waves, the waves' partial tiles added in wave
+// order (deterministic).  fp32 inputs, fp64 products (exact) and sums: the
+// node-by-node fp64 loop it replaces summed in another order, so results move
+// by fp64 rounding only (~1e-16 relative).  The loop made one dependent LDS /
+// HBM round trip per node: ~60 us of every v3 slice prologue at config 3 and
+// ~1.4 ms of every kind-22 launch at config 5's rank shape.
+//
+// Output: gram[kk(a) * ks + kk(b)] = G[a][b] for a, b < M2, both triangles,
+// where kk(a) = the state row whose J entry is column a (row U_c carries V_c:
+// kk(R + c) = 2 + c, kk(c) = 2 + R + c); colsum[a] = sum_{j>=1} x_ja;
+// x0[a] = node 0's entry.  All threads of the workgroup call it (barriers).
+typedef double ame_p0d4 __attribute__((ext_vector_type(4)));
+template <int R, int NW>
+__device__ __forceinline__ void p0_gram_mfma(const float* xo, int n, int D, double* gram, int ks,
+                                             double* colsum, float* x0) {
+    constexpr int M2 = 2 * R, NT = (M2 + 15) / 16, NTL = NT * (NT + 1) / 2;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int ci = lane & 15, ck = lane >> 4;
+    ame_p0d4 acc[NTL];
+#pragma unroll
+    for (int t = 0; t < NTL; ++t) acc[t] = ame_p0d4{0.0, 0.0, 0.0, 0.0};
+    double cs[NT];
+#pragma unroll
+    for (int I = 0; I < NT; ++I) cs[I] = 0.0;
+    const int nch = (n + 3) / 4;
+    constexpr int U = 4;   // chunks whose loads are issued together
+    for (int c0 = w; c0 < nch; c0 += NW * U) {
+        float xv[U][NT];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = 4 * (c0 + NW * u) + ck;
+#pragma unroll
+            for (int I = 0; I < NT; ++I) {
+                const int col = 16 * I + ci;
+                const bool ok = j >= 1 && j < n && col < M2;
+                xv[u][I] = ok ? xo[(size_t)j * D + 2 + col] : 0.f;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            double xd[NT];
+#pragma unroll
+            for (int I = 0; I < NT; ++I) {
+                xd[I] = (double)xv[u][I];
+                cs[I] += xd[I];
+            }
+#pragma unroll
+            for (int I = 0; I < NT; ++I)
+#pragma unroll
+                for (int J = 0; J <= I; ++J) {
+                    const int t = I * (I + 1) / 2 + J;
+                    acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(xd[I], xd[J], acc[t], 0, 0, 0);
+                }
+        }
+    }
+    // column sums: the 4 node lanes of a column, fixed tree
+#pragma unroll
+    for (int I = 0; I < NT; ++I) {
+        const double s1 = cs[I] + __shfl_xor(cs[I], 16);
+        cs[I] = s1 + __shfl_xor(s1, 32);
+    }
+    auto kk = [](int a) { return 2 + (a >= R ? a - R : a + R); };
+    for (int ww = 0; ww < NW; ++ww) {
+        if (w == ww) {
+#pragma unroll
+            for (int I = 0; I < NT; ++I)
+#pragma unroll
+                for (int J = 0; J <= I; ++J) {
+                    const int t = I * (I + 1) / 2 + J;
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) {
+                        const int a = 16 * I + ck + 4 * v, b = 16 * J + ci;
+                        if (a >= M2 || b >= M2) continue;
+                        double* p = gram + kk(a) * ks + kk(b);
+                        double* q = gram + kk(b) * ks + kk(a);
+                        const double g = acc[t][v];
+                        *p = (ww == 0) ? g : *p + g;
+                        if (I != J) *q = *p;
+                    }
+                }
+            if (ck == 0) {
+#pragma unroll
+                for (int I = 0; I < NT; ++I) {
+                    const int a = 16 * I + ci;
+                    if (a < M2) colsum[a] = (ww == 0) ? cs[I] : colsum[a] + cs[I];
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (tid < M2) x0[tid] = xo[2 + tid];
+    __syncthreads();
 }
 
 // LDS-DMA: each lane's 16 (4) bytes from gsrc land at LDS byte lds + lane*16 (*4).
