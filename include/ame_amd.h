@@ -248,6 +248,12 @@ long long ame_sweep_work_size(const ame_dims* dims, int kind);
  * workgroups alone (workers are then used when they fit, ame_sweep_kind). */
 int ame_sweep_max_slices(int n, int r, int request);
 
+/* Workgroups one slice occupies in a launch of a concrete kind (the slice's
+ * own plus its GEMV workers; each is one CU's worth of LDS), -1 for a request
+ * or an unknown kind.  A caller that confines the sweep to a CU range
+ * (ame_stream_create_cu_range) sizes the launch with it. */
+int ame_sweep_slice_workgroups(int kind);
+
 /* Dynamic LDS bytes per slice workgroup of a concrete kind (0 = unsupported). */
 long long ame_sweep_lds_bytes(int n, int r, int kind);
 

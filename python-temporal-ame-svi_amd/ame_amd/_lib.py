@@ -66,7 +66,7 @@ class ame_elbo_args(ctypes.Structure):
 
 
 # every symbol include/ame_amd.h declares (checked by tests/test_capi.py)
-EXPORTS = ("ame_pack_y", "ame_pack_y_size", "ame_sweep", "ame_sweep_kind", "ame_sweep_work_size", "ame_sweep_orders_slices", "ame_sweep_max_slices", "ame_sweep_lds_bytes", "ame_cov",
+EXPORTS = ("ame_pack_y", "ame_pack_y_size", "ame_sweep", "ame_sweep_kind", "ame_sweep_work_size", "ame_sweep_orders_slices", "ame_sweep_max_slices", "ame_sweep_slice_workgroups", "ame_sweep_lds_bytes", "ame_cov",
            "ame_elbo", "ame_elbo_work_size", "ame_elbo_pairs_diag", "ame_host_register", "ame_host_unregister",
            "ame_stream_create_cu_range", "ame_stream_destroy",
            "ame_peer_alloc", "ame_peer_free", "ame_peer_open", "ame_peer_close",
@@ -100,6 +100,8 @@ def _declare(L):
     if hasattr(L, "ame_debug_occupy"):   # diagnostic; absent from older A/B builds
         L.ame_debug_occupy.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint, c_vp, c_vp]
         L.ame_debug_occupy.restype = ctypes.c_int
+    L.ame_sweep_slice_workgroups.argtypes = [ctypes.c_int]
+    L.ame_sweep_slice_workgroups.restype = ctypes.c_int
     L.ame_sweep_orders_slices.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
     L.ame_sweep_orders_slices.restype = ctypes.c_int
     L.ame_sweep_kind.argtypes = [P(ame_dims), ctypes.c_int]

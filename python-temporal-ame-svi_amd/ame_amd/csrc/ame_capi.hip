@@ -309,6 +309,18 @@ int ame_sweep_max_slices(int n, int r, int request) {
     }
 }
 
+int ame_sweep_slice_workgroups(int kind) {
+    switch (kind) {
+        case AME_SWEEP_V3:
+        case AME_SWEEP_V2_LDS:
+        case AME_SWEEP_V2_HBM: return 1;
+        case AME_SWEEP_V2_WORKERS: return 1 + ame_v2_nworkers(2);
+        case AME_SWEEP_V2_PIPE: return 1 + ame_v2_nworkers(3);
+        case AME_SWEEP_V2_W6: return 1 + ame_v2_nworkers(4);
+        default: return fail("ame_sweep_slice_workgroups: %d is not a concrete sweep kind", kind);
+    }
+}
+
 int ame_sweep_orders_slices(int n, int r, int kind) {
     if (!r_supported(r) || n < 2) return 0;
     if (kind == AME_SWEEP_V3) return ame_sweep3_supported(n, r) ? 1 : 0;

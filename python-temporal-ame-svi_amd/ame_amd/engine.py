@@ -330,9 +330,12 @@ class DeviceEngine:
         self._cu_split = None
         if opt.elbo_cus:
             # ELBO beside the sweep: the sweep's launch must fit the CUs left to it
-            per_slice = {_lib.AME_SWEEP_V2_WORKERS: 8, _lib.AME_SWEEP_V2_W6: 7}.get(opt.sweep_kernel)
+            # (workgroups per slice from the library, one CU each)
+            per_slice = None
+            if opt.sweep_kernel in (_lib.AME_SWEEP_V2_WORKERS, _lib.AME_SWEEP_V2_W6):
+                per_slice = int(self.L.ame_sweep_slice_workgroups(opt.sweep_kernel))
             cus = int(torch.cuda.get_device_properties(self.dev).multi_processor_count)
-            if per_slice is None or not 0 < int(opt.elbo_cus) < cus:
+            if per_slice is None or per_slice < 1 or not 0 < int(opt.elbo_cus) < cus:
                 raise ValueError("elbo_cus needs sweep_kernel 22 or 24 and 0 < elbo_cus < "
                                  f"{cus} CUs (got {opt.elbo_cus}, kernel {opt.sweep_kernel})")
             self.max_slices = min(self.max_slices, (cus - int(opt.elbo_cus)) // per_slice)

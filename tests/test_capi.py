@@ -58,6 +58,9 @@ def test_host_only_entry_points():
     assert lib.ame_sweep_work_size(ctypes.byref(d), L.AME_SWEEP_V2_HBM) == 128 * 1024 * 32 // 2
     assert lib.ame_sweep_work_size(ctypes.byref(d), L.AME_SWEEP_V2_WORKERS) == 128 * 7 * 8 * 34 + 128 * 1024 * 4 * 34
     assert lib.ame_sweep_work_size(ctypes.byref(d), 2) == -1     # a request, not a kind
+    # workgroups per slice (the engine's elbo_cus sizing reads these)
+    assert [lib.ame_sweep_slice_workgroups(k) for k in (3, 20, 21, 22, 23, 24)] == [1, 1, 1, 8, 5, 7]
+    assert lib.ame_sweep_slice_workgroups(L.AME_SWEEP_AUTO) == -1
 
 
 def test_worker_partial_tag_never_zero():
