@@ -442,6 +442,10 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true",
                     help="sweeps in order (profiling: per-dispatch counters without the "
                          "pipelined launches' waiting)")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="process-group backend under torchrun (nccl = RCCL, the production "
+                         "path; gloo rehearses the multi-rank bench with several ranks on one GPU, "
+                         "where RCCL refuses two ranks per device)")
     ap.add_argument("--force-dist", action="store_true",
                     help="use the process group (nccl) and the time-sharded path even at world size 1 "
                          "(checks RCCL initialisation on a one-GPU box)")
@@ -483,7 +487,10 @@ def main():
         print(json.dumps(out), file=json_out, flush=True)
         return out
     if use_dist:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     from ame_amd import TemporalAMEModel, TemporalAMENaiveMFVI, TemporalAMEStructuredMFVI
 
@@ -530,7 +537,8 @@ def main():
     per_rank_ms = [dt / args.steps * 1e3]
     per_rank_cross = [cross_ms]
     if use_dist:
-        tt = torch.tensor([dt, cross_ms[0], cross_ms[1]], dtype=torch.float64, device=dev)
+        tt = torch.tensor([dt, cross_ms[0], cross_ms[1]], dtype=torch.float64,
+                          device=dev if args.dist_backend == "nccl" else "cpu")
         allt = [torch.zeros_like(tt) for _ in range(world)]
         dist.all_gather(allt, tt)
         per_rank_ms = [float(x[0].item()) / args.steps * 1e3 for x in allt]

@@ -100,8 +100,9 @@ def _declare(L):
     if hasattr(L, "ame_debug_occupy"):   # diagnostic; absent from older A/B builds
         L.ame_debug_occupy.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint, c_vp, c_vp]
         L.ame_debug_occupy.restype = ctypes.c_int
-    L.ame_sweep_slice_workgroups.argtypes = [ctypes.c_int]
-    L.ame_sweep_slice_workgroups.restype = ctypes.c_int
+    if hasattr(L, "ame_sweep_slice_workgroups"):   # absent from older A/B builds only
+        L.ame_sweep_slice_workgroups.argtypes = [ctypes.c_int]
+        L.ame_sweep_slice_workgroups.restype = ctypes.c_int
     L.ame_sweep_orders_slices.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
     L.ame_sweep_orders_slices.restype = ctypes.c_int
     L.ame_sweep_kind.argtypes = [P(ame_dims), ctypes.c_int]

@@ -1,6 +1,6 @@
 """Build a one-latent-dim variant library for same-box A/B runs (tools/ab_v3.py).
 
-    python tools/build_variant.py --r=16 --tag=X [--defs=A,B]   -> tools/_lib/libame_amd_X.so
+    python tools/build_variant.py --r=16 --tag=X [--defs=A,B] [--flags=-f1,-f2]   -> tools/_lib/libame_amd_X.so
 
 Unsplit sources, -DAME_ONLY_R=<r>, plus -D<def> for each listed switch.  A
 variant library is a diagnostic: it is never the product build (build.py)."""
@@ -28,6 +28,7 @@ def main():
     r = int(_opt("--r", 16))
     tag = _opt("--tag", f"r{r}")
     defs = [f"-D{d}" for d in (_opt("--defs") or "").split(",") if d]
+    defs += [f for f in (_opt("--flags") or "").split(",") if f]   # extra compiler flags
     os.makedirs(BDIR, exist_ok=True)
     os.makedirs(LIBDIR, exist_ok=True)
     csrc = os.path.join(PKG, "ame_amd", "csrc")
