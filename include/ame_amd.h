@@ -133,6 +133,10 @@ enum ame_sweep_kind_code {
 #define AME_SWEEP_FLAG_NEXT_GROUP 1u   /* done[T_local] is the next slice group's first slice
                                           (same rank): with wait_epoch, the last slice also
                                           waits for it, as for any other right neighbour */
+#define AME_SWEEP_FLAG_PREV_GROUP 2u   /* halo_in is the previous slice group's hand-off
+                                          buffer on this GPU, not a neighbouring rank's: the
+                                          first slice's wait on it is a local wait (2 s
+                                          budget, not counted in status words 9 / 11) */
 
 /* ELBO pair kernels (ame_elbo_args.pairs_kernel): AUTO = V2 (LDS-DMA rows). */
 enum ame_pairs_kernel_code { AME_PAIRS_AUTO = 0, AME_PAIRS_V1 = 1, AME_PAIRS_V2 = 2 };

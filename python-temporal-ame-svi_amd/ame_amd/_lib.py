@@ -32,6 +32,7 @@ AME_PEER_HANDLE_BYTES = 64
 AME_SWEEP_AUTO, AME_SWEEP_V2_SINGLE, AME_SWEEP_V2_AUTO, AME_SWEEP_V3 = 0, 1, 2, 3
 AME_SWEEP_V2_LDS, AME_SWEEP_V2_HBM, AME_SWEEP_V2_WORKERS, AME_SWEEP_V2_PIPE, AME_SWEEP_V2_W6 = 20, 21, 22, 23, 24
 AME_SWEEP_FLAG_NEXT_GROUP = 1
+AME_SWEEP_FLAG_PREV_GROUP = 2
 # ELBO pair kernels (enum ame_pairs_kernel_code)
 AME_PAIRS_AUTO, AME_PAIRS_V1, AME_PAIRS_V2 = 0, 1, 2
 

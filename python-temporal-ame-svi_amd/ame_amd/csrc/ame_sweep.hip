@@ -1095,8 +1095,10 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     // wave 1: wait for the granules of mu_{node,t-1}^new (returns when done or timed out);
     // lane L owns state rows L + 64h
     auto poll_left = [&](int node, const uint64_t (&first)[KH]) {
-        const bool from_halo = (tl == 0);
-        const uint64_t* src = from_halo ? a.halo_in + (size_t)node * D
+        // halo_in: the left rank's peer buffer, or (AME_SWEEP_FLAG_PREV_GROUP) the
+        // previous slice group's granules on this GPU -- then a local wait
+        const bool from_halo = (tl == 0) && !(a.flags & AME_SWEEP_FLAG_PREV_GROUP);
+        const uint64_t* src = (tl == 0) ? a.halo_in + (size_t)node * D
                                         : a.hand + ((size_t)(tl - 1) * n + node) * D;
         uint64_t v[KH];
         bool ok = true;
@@ -1149,8 +1151,8 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
             }
     };
     auto first_poll = [&](int node, uint64_t (&g)[KH]) {   // wave 1: issue the first granule loads
-        const bool from_halo = (tl == 0);
-        const uint64_t* src = from_halo ? a.halo_in + (size_t)node * D
+        const bool from_halo = (tl == 0) && !(a.flags & AME_SWEEP_FLAG_PREV_GROUP);
+        const uint64_t* src = (tl == 0) ? a.halo_in + (size_t)node * D
                                         : a.hand + ((size_t)(tl - 1) * n + node) * D;
 #pragma unroll
         for (int h = 0; h < KH; ++h) {

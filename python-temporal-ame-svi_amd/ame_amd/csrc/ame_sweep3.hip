@@ -265,7 +265,9 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
         }
         bool ok = (lane >= D) || (uint32_t)(v >> 32) == a.epoch;
         if (!__all(ok) && !dead) {
-            const bool cross = tl == 0;
+            // the left rank, or (AME_SWEEP_FLAG_PREV_GROUP) the previous slice group
+            // on this GPU: a local wait then
+            const bool cross = tl == 0 && !(a.flags & AME_SWEEP_FLAG_PREV_GROUP);
             AmeSpin w(a.status, cross, lane == 0, hw == 0 ? AME_ST_HALO_US : 0);   // hw 0-2 wait alike
             const uint64_t* src = gran_src(node);
             while (true) {

@@ -649,7 +649,8 @@ class DeviceEngine:
                 cov_new=at(self.covs[dst], off, ndd, 4), done=at(self.done, off, 1, 4),
                 wait_epoch=wait, back_out=back_out if g == 0 else None,
                 back_in=back_in if g == last else None,
-                flags=_lib.AME_SWEEP_FLAG_NEXT_GROUP if g < last else 0)
+                flags=(_lib.AME_SWEEP_FLAG_NEXT_GROUP if g < last else 0)
+                | (_lib.AME_SWEEP_FLAG_PREV_GROUP if g > 0 else 0))
             _lib.check(self.L.ame_sweep(ctypes.byref(dims), ctypes.byref(a),
                                         ctypes.c_void_p(stream.cuda_stream)), "ame_sweep")
         self._toc(tok, stream)
