@@ -35,6 +35,7 @@ from __future__ import annotations
 
 import atexit
 import ctypes
+import os
 import socket
 from typing import Optional, Tuple
 
@@ -85,12 +86,87 @@ class PeerBuffer:
         self.dev = None
 
 
-class TimeShardHalo:
-    """Halo exchange for one engine (rank) of a time-sharded run."""
+class HostPeerBuffer:
+    """The host-memory form of a peer buffer: a POSIX shared-memory file
+    (/dev/shm) mapped into each process and registered for device access
+    (ame_host_register: hipHostRegister, mapped + portable), so the neighbour's
+    system-scope stores and this rank's system-scope polls meet in host memory
+    instead of in the owner's HBM.  The fallback when the device-IPC peer link
+    fails its pre-flight (TimeShardHalo peer_mode "auto"); slower per poll
+    (host memory over the fabric), same protocol, same results."""
 
-    def __init__(self, shard: Shard, group=None):
+    def __init__(self, nbytes: int = 0, handle=None):
+        import mmap
+        import uuid
+        L = _lib.lib()
+        self.dev = ctypes.c_void_p()
+        if handle is None:
+            name = f"/dev/shm/ame_amd_{os.getpid()}_{uuid.uuid4().hex[:12]}"
+            fd = os.open(name, os.O_CREAT | os.O_EXCL | os.O_RDWR, 0o600)
+            os.ftruncate(fd, nbytes)      # zero-filled
+            self.owner = True
+        else:
+            name, nbytes = handle
+            fd = os.open(name, os.O_RDWR)
+            self.owner = False
+        try:
+            self._mm = mmap.mmap(fd, nbytes)
+        finally:
+            os.close(fd)
+        self._path, self._bytes = name, nbytes
+        self._cbuf = (ctypes.c_char * nbytes).from_buffer(self._mm)
+        self._host = ctypes.c_void_p(ctypes.addressof(self._cbuf))
+        try:
+            _lib.check(L.ame_host_register(self._host, nbytes, ctypes.byref(self.dev)),
+                       "ame_host_register")
+        except Exception:
+            self._release(register=False)
+            raise
+        self.handle = (name, nbytes)
+
+    def _release(self, register=True):
+        if register:
+            try:
+                _lib.lib().ame_host_unregister(self._host)
+            except Exception:
+                pass
+        self._cbuf = None
+        try:
+            self._mm.close()
+        except Exception:
+            pass
+        if self.owner:
+            try:
+                os.unlink(self._path)
+            except OSError:
+                pass
+
+    def close(self):
+        if self.dev is None:
+            return
+        self._release()
+        self.dev = None
+
+
+class TimeShardHalo:
+    """Halo exchange for one engine (rank) of a time-sharded run.
+
+    peer_mode: "ipc" -- the peer buffers live in the polling rank's HBM and the
+    neighbour maps them over device IPC (xGMI stores); "host" -- POSIX shared
+    host memory registered on both devices (HostPeerBuffer); "auto" (default)
+    -- ipc, and host when the ipc links fail their pre-flight on any rank (every
+    rank then switches, so all ranks use one mode)."""
+
+    PEER_MODES = ("auto", "ipc", "host")
+
+    def __init__(self, shard: Shard, group=None, peer_mode: str = "auto"):
+        if peer_mode not in self.PEER_MODES:
+            raise ValueError(f"peer_mode must be one of {self.PEER_MODES}, got {peer_mode!r}")
         self.shard = shard
         self.group = group
+        self.peer_mode = peer_mode
+        self.peer_kind = None    # "ipc" or "host" once the links passed their pre-flight
+        self.preflight_log = []  # failures of a mode that was given up ("auto")
         self._peers = None       # (own halo, own back, peer halo, peer back) PeerBuffers
         self._next_old = None
         self._prev_final = None
@@ -102,17 +178,17 @@ class TimeShardHalo:
         return t.cpu() if (self._host_coll and t.is_cuda) else t
 
     @classmethod
-    def create(cls, T: int, group=None) -> "TimeShardHalo":
+    def create(cls, T: int, group=None, peer_mode: str = "auto") -> "TimeShardHalo":
         world = dist.get_world_size(group)
         rank = dist.get_rank(group)
         t0, tl = shard_range(T, world, rank)
-        return cls(Shard(t0, tl, T, rank, world), group)
+        return cls(Shard(t0, tl, T, rank, world), group, peer_mode)
 
     # ---- setup (called once the engine knows n, d) ----
     def _setup(self, eng):
         if self._peers is not None or self.shard.world == 1:
             return
-        rank, world = self.shard.rank, self.shard.world
+        world = self.shard.world
         hosts = [None] * world
         dist.all_gather_object(hosts, socket.gethostname(), group=self.group)
         if len(set(hosts)) != 1:
@@ -121,19 +197,51 @@ class TimeShardHalo:
                 f"must all run on one node; got hosts {sorted(set(hosts))}")
         nd = eng.n * eng.d
         self._back_bytes = (((nd + 63) // 64) * 64 + 64) * 4      # floats + done word
+        kinds = {"auto": ("ipc", "host"), "ipc": ("ipc",), "host": ("host",)}[self.peer_mode]
+        for i, kind in enumerate(kinds):
+            try:
+                self._setup_kind(eng, kind)
+                self.peer_kind = kind
+                break
+            except Exception as e:   # noqa: BLE001 -- every rank raised alike (pre-flight)
+                if i + 1 == len(kinds):
+                    raise
+                self.preflight_log.append(f"{kind}: {e}")
+        atexit.register(self.close)
+
+    def _setup_kind(self, eng, kind: str):
+        """Allocate / map the four peer buffers of one kind and pre-flight them.
+        Allocation and mapping failures are recorded, not raised, so every rank
+        reaches the pre-flight's barrier and all_reduce and raises together."""
+        rank, world = self.shard.rank, self.shard.world
+        nd = eng.n * eng.d
+        Buf = PeerBuffer if kind == "ipc" else HostPeerBuffer
+        pre_bad = []
+
+        def make(what, **kw):
+            try:
+                return Buf(**kw)
+            except Exception as e:   # noqa: BLE001 -- reported on every rank by the pre-flight
+                pre_bad.append(f"rank {rank}: {kind} {what}: {e}")
+                return None
         with torch.cuda.device(eng.dev):
             # buffers this rank POLLS: its left halo (granules from rank-1) and the
             # back channel of its right boundary (final means of rank+1's first slice)
-            own_halo = PeerBuffer(nd * 8) if rank > 0 else None
-            own_back = PeerBuffer(self._back_bytes) if rank < world - 1 else None
+            own_halo = make("left halo", nbytes=nd * 8) if rank > 0 else None
+            own_back = make("back channel", nbytes=self._back_bytes) if rank < world - 1 else None
             mine = (own_halo.handle if own_halo else None, own_back.handle if own_back else None)
             allh = [None] * world
             dist.all_gather_object(allh, mine, group=self.group)
-            peer_halo = PeerBuffer(handle=allh[rank + 1][0]) if rank < world - 1 else None
-            peer_back = PeerBuffer(handle=allh[rank - 1][1]) if rank > 0 else None
+            peer_halo = peer_back = None
+            if rank < world - 1 and allh[rank + 1][0] is not None:
+                peer_halo = make("map of the right rank's halo", handle=allh[rank + 1][0])
+            if rank > 0 and allh[rank - 1][1] is not None:
+                peer_back = make("map of the left rank's back channel", handle=allh[rank - 1][1])
+            if (rank < world - 1 and peer_halo is None) or (rank > 0 and peer_back is None):
+                pre_bad.append(f"rank {rank}: {kind}: a neighbour's buffer is missing")
         peers = (own_halo, own_back, peer_halo, peer_back)
         try:
-            self._preflight(eng, peers)
+            self._preflight(eng, peers, pre_bad=pre_bad, mode=kind)
         except Exception:
             # nothing may sweep over a link that failed: _peers stays unset, so a
             # caller that catches this and fits again re-runs the setup (and the
@@ -143,7 +251,6 @@ class TimeShardHalo:
                     p.close()
             raise
         self._peers = peers
-        atexit.register(self.close)
 
     @staticmethod
     def _sentinel(kind: int, writer: int, owner: int) -> int:
@@ -151,20 +258,21 @@ class TimeShardHalo:
         # up from 1), and the buffers are zeroed again after the check
         return ((0xA3E50000 | (kind << 12) | (writer & 0xFFF)) << 32) | (owner & 0xFFFFFFFF)
 
-    def _preflight(self, eng, peers, wait_s: float = 2.0):
+    def _preflight(self, eng, peers, wait_s: float = 2.0, pre_bad=None, mode: str = "ipc"):
         """Every peer link once, before the first sweep: each rank stores a
         sentinel into each buffer it MAPPED (the right neighbour's halo, the left
         neighbour's back channel) with the same system-scope store the sweep's
         hand-off uses, from its own device; after a barrier every owner reads
         its buffers back.  A missing or wrong value raises naming the rank pair
         and the link, instead of the first sweep spinning until the status word
-        reports a halo timeout.  Reference: structured_mf.py:240 (the T loop
-        whose boundary the links carry)."""
+        reports a halo timeout.  pre_bad: failures of the buffers' allocation /
+        mapping (raised here, on every rank alike).  Reference:
+        structured_mf.py:240 (the T loop whose boundary the links carry)."""
         import time
         L = _lib.lib()
         rank = self.shard.rank
         own_halo, own_back, peer_halo, peer_back = peers
-        bad = []
+        bad = list(pre_bad or [])
 
         def call(fn, *args, what):
             # a library error is recorded, never raised here: every rank must
@@ -212,10 +320,10 @@ class TimeShardHalo:
         dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
         if bad:
             msg = L.ame_last_error().decode(errors="replace")
-            raise RuntimeError("ame_amd: peer-link pre-flight failed: " + "; ".join(bad) +
+            raise RuntimeError(f"ame_amd: peer-link pre-flight ({mode}) failed: " + "; ".join(bad) +
                                f" (last library message: {msg!r})")
         if int(flag.item()):
-            raise RuntimeError("ame_amd: peer-link pre-flight failed on another rank")
+            raise RuntimeError(f"ame_amd: peer-link pre-flight ({mode}) failed on another rank")
         self.preflight_ok = True
 
     def quiesce(self, eng):

@@ -104,7 +104,8 @@ class DeviceTemporalVI(BaseTemporalVariationalInference):
         if not use:
             return None, None
         from ..distributed import TimeShardHalo
-        halo = TimeShardHalo.create(self.T)
+        # distributed=True / None: defaults; a dict: TimeShardHalo options (peer_mode)
+        halo = TimeShardHalo.create(self.T, **(use if isinstance(use, dict) else {}))
         return halo.shard, halo
 
     def _ensure_engine(self) -> DeviceEngine:

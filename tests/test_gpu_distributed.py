@@ -43,12 +43,17 @@ def _run(n, T, r, method, lr, iters, distributed, depth=None, kind=None):
     opts = {} if depth is None else {"spec_depth": depth}
     if kind == P23:   # requested: AUTO picks kind 22 for these shapes
         opts["sweep_kernel"] = P23
+    # distributed: True, or TimeShardHalo options plus "expect" (the peer kind
+    # the links must end up with)
+    dopt = distributed
+    if isinstance(distributed, dict):
+        dopt = {k: v for k, v in distributed.items() if k != "expect"}
     if method == "naive":
-        vi = TemporalAMENaiveMFVI(m, learning_rate=lr, device=dev, distributed=distributed,
+        vi = TemporalAMENaiveMFVI(m, learning_rate=lr, device=dev, distributed=dopt,
                                   engine_options=opts)
     else:
         vi = TemporalAMEStructuredMFVI(m, factorization=method, learning_rate=lr, device=dev,
-                                       distributed=distributed, engine_options=opts)
+                                       distributed=dopt, engine_options=opts)
     eng = vi.engine
     if kind is not None:
         assert eng.sweep_kind == kind, (eng.sweep_kind, kind)
@@ -57,16 +62,19 @@ def _run(n, T, r, method, lr, iters, distributed, depth=None, kind=None):
     h = vi.fit(max_iter=iters, tolerance=0.0, verbose=False)
     if distributed:   # every peer link passed the setup pre-flight (distributed.py)
         assert vi._halo.preflight_ok
+        if isinstance(distributed, dict):
+            want = distributed.get("expect", distributed.get("peer_mode"))
+            assert vi._halo.peer_kind == want, (vi._halo.peer_kind, want, vi._halo.preflight_log)
     return (vi.X_mean.numpy().copy(), vi.X_cov.numpy().copy(),
             [float(e) for e in h["elbo"]], list(h["reconstruction_error"]))
 
 
-def _worker(rank, world, port, args, q):
+def _worker(rank, world, port, args, q, dist_opt=True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         n, T, r, method, lr, iters, depth, kind = args
-        out = _run(n, T, r, method, lr, iters, True, depth, kind)
+        out = _run(n, T, r, method, lr, iters, dist_opt, depth, kind)
         if rank == 0:
             q.put(out)
     finally:
@@ -91,13 +99,28 @@ def _worker(rank, world, port, args, q):
     (2, 300, 8, 32, "good", 0.5, 5, None, P23), (3, 240, 12, 32, "bad", 0.7, 6, 3, P23),
     (2, 200, 6, 32, "naive", 0.4, 5, None, P23)])
 def test_ranks_one_gpu(world, n, T, r, method, lr, iters, depth, kind):
+    _ranks_vs_one_process(world, n, T, r, method, lr, iters, depth, kind, True)
+
+
+@pytest.mark.parametrize("world,n,T,r,method,lr,iters,depth,kind", [
+    (2, 64, 8, 4, "good", 0.5, 3, None, V3), (3, 60, 12, 4, "good", 0.5, 8, 3, V3),
+    (2, 300, 8, 32, "good", 0.5, 3, None, W22), (2, 300, 8, 32, "bad", 0.5, 5, None, P23)])
+def test_ranks_host_peer_buffers(world, n, T, r, method, lr, iters, depth, kind):
+    """peer_mode "host" (distributed.py HostPeerBuffer, the fallback when the
+    device-IPC links fail their pre-flight): halo granules and back channels in
+    POSIX shared host memory registered on the device; bit-equal to one
+    process like the IPC form."""
+    _ranks_vs_one_process(world, n, T, r, method, lr, iters, depth, kind, {"peer_mode": "host"})
+
+
+def _ranks_vs_one_process(world, n, T, r, method, lr, iters, depth, kind, dist_opt):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     args = (n, T, r, method, lr, iters, depth, kind)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(rk, world, port, args, q)) for rk in range(world)]
+    procs = [ctx.Process(target=_worker, args=(rk, world, port, args, q, dist_opt)) for rk in range(world)]
     for p in procs:
         p.start()
     try:
@@ -213,3 +236,53 @@ def test_preflight_detects_bad_link():
     # the failing probe: rank 1 names the call, rank 0 sees its back channel empty
     assert got2[1] is not None and "ame_peer_probe" in got2[1], got2[1]
     assert got2[0] is not None and "rank 1 -> rank 0 (back channel)" in got2[0], got2[0]
+
+
+def _fallback_worker(rank, world, port, q):
+    """peer_mode "auto" with the device-IPC buffers made to fail on rank 1: the
+    ipc pre-flight raises on both ranks, both switch to host buffers."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import ame_amd.distributed as D
+        if rank == 1:
+            class _NoIpc(D.PeerBuffer):
+                def __init__(self, *a, **k):
+                    raise RuntimeError("injected: device IPC unavailable")
+            D.PeerBuffer = _NoIpc
+        out = _run(64, 8, 4, "good", 0.5, 3, {"peer_mode": "auto", "expect": "host"})
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ipc_failure_falls_back_to_host_buffers():
+    """The auto peer mode: a rank whose device-IPC buffer cannot be made records
+    it, the ipc pre-flight fails on EVERY rank (no rank sweeps over a half-made
+    link), every rank switches to host buffers, and the fit is bit-equal to one
+    process."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fallback_worker, args=(rk, 2, port, q)) for rk in range(2)]
+    for p in procs:
+        p.start()
+    outs = {}
+    try:
+        for _ in range(2):
+            rk, out = q.get(timeout=150)
+            outs[rk] = out
+    except Exception:
+        pass
+    for p in procs:
+        p.join(timeout=30)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.exitcode is None:
+            p.kill()
+            p.join()
+    assert codes == [0, 0], f"rank exit codes {codes}"
+    mean_s, cov_s, _, _ = _run(64, 8, 4, "good", 0.5, 3, False)
+    assert np.array_equal(outs[0][0], mean_s) and np.array_equal(outs[0][1], cov_s)
