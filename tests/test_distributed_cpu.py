@@ -135,3 +135,39 @@ def test_time_sharded_sweep_matches_unsharded(n, T, r, method, lr):
     got = [terms["loglik"], terms["prior0"], terms["trans"], terms["entropy"]]
     assert np.allclose(got, ref, rtol=1e-12, atol=1e-9)
     assert abs(terms["recon"] - O.recon_error(Y, Xm)) < 1e-12
+
+
+def _sharers_worker(rank, world, port, same, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ame_amd.distributed import TimeShardHalo
+        halo = TimeShardHalo.create(8 * world)
+        # the device identity of each rank (host, PCI address, UUID) without a
+        # GPU: every rank on one device, or ranks 0-1 / 2-3 on two devices
+        halo.device_key = staticmethod(lambda dev: ("h", 0, 0 if same else rank // 2, 0, ""))
+
+        class _Eng:
+            dev = None
+        q.put((rank, halo.device_sharers(_Eng()), halo.peer_mode))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("same", [True, False])
+def test_device_sharers_counts_ranks_per_gpu(same):
+    """TimeShardHalo.device_sharers (the engine's co-residency budget divisor,
+    DESIGN.md §5): 4 gloo ranks, all on one device -> 4 each; two per device
+    -> 2 each.  The default peer mode is "auto" (IPC, host fallback)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharers_worker, args=(rk, 4, port, same, q)) for rk in range(4)]
+    for p in procs:
+        p.start()
+    got = dict((rk, (k, m)) for rk, k, m in (q.get(timeout=120) for _ in range(4)))
+    for p in procs:
+        p.join(timeout=30)
+    assert [p.exitcode for p in procs] == [0] * 4
+    assert all(m == "auto" for _, m in got.values())
+    assert [got[r][0] for r in range(4)] == ([4] * 4 if same else [2] * 4)

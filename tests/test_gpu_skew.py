@@ -175,3 +175,32 @@ def ctypes_ptr(t):
 def ctypes_stream(s):
     import ctypes
     return ctypes.c_void_p(s.cuda_stream)
+
+
+def test_starved_sweep_raises_one_record(gpu_device):
+    """The other side of the co-residency edge: a foreign kernel holds 200 CUs
+    for 3.5 s, longer than the 2 s local budget, while config 3's 128-slice
+    sweep starts.  The slices that did get a CU wait on neighbours that did not;
+    the first wait to outlive its budget raises SPIN_TIMEOUT with its record,
+    and every later wait gives up quietly -- one bit, one record, no second
+    status manufactured by the first (include/ame_amd.h wait rules)."""
+    import ame_amd._lib as L
+    dev = gpu_device
+    vi = _vi(_model(dev), dev)
+    eng = vi.engine
+    lib = L.lib()
+    touched = torch.zeros(1, dtype=torch.int32, device=dev)
+    hog = torch.cuda.Stream(device=dev)
+    torch.cuda.synchronize(dev)
+    assert lib.ame_debug_occupy(200, 160 * 1024, 3_500_000, ctypes_ptr(touched), ctypes_stream(hog)) == 0
+    with pytest.raises(RuntimeError) as ei:
+        vi.fit(max_iter=3, tolerance=0.0, verbose=False)
+    torch.cuda.synchronize(dev)
+    msg = str(ei.value)
+    print(msg)
+    w = [x & 0xFFFFFFFF for x in eng.last_status]
+    # one bit: the slice-to-slice wait (or, if a helper's spin outlasts the
+    # solver's, the LDS counter behind it) -- never both
+    assert w[0] in (L.AME_STATUS_SPIN_TIMEOUT, L.AME_STATUS_LDS_TIMEOUT), w
+    assert w[1] == 1 and w[2] in L.AME_WAIT_SITES and w[7] >= 2_000_000, w
+    assert "first failure:" in msg

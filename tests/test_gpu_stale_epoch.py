@@ -84,10 +84,20 @@ def test_stale_done_flag_is_reported_not_consumed(gpu_device):
     eng._order_after_host_writes = False     # the hole the engine closes
     _poisoned_pending_zero(eng)
     try:
-        with pytest.raises(RuntimeError, match="epoch outside the protocol"):
+        with pytest.raises(RuntimeError, match="epoch outside the protocol") as ei:
             vi.fit(max_iter=3, tolerance=0.0, verbose=False)
     finally:
         torch.cuda.synchronize()
+    # the status block's record (include/ame_amd.h): one bit -- the waits behind
+    # the first failure gave up quietly -- and the first wait's site, the
+    # poisoned word it saw and the epoch it waited for
+    w = [x & 0xFFFFFFFF for x in eng.last_status]
+    print(str(ei.value))
+    assert w[0] == 8, w                       # AME_STATUS_STALE_EPOCH only
+    assert w[1] == 1 and w[2] in (1, 2), w    # done flag of slice t / t+1
+    assert w[5] == POISON and 1 <= w[6] < POISON and w[8] == w[6] + 1, w
+    assert 0 <= w[3] < SHAPE[1] and w[4] == 0xFFFFFFFF, w   # a slice, in the prologue
+    assert "first failure: done flag of slice" in str(ei.value)
 
 
 def test_process_epochs_increase_across_engines(gpu_device):
