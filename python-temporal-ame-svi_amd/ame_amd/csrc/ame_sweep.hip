@@ -565,7 +565,10 @@ struct Ph3 {
     static_assert(NBT <= AME_NT, "phase-3 blocks exceed the workgroup");
 };
 
-template <int R, int MODE>
+// VAR: the factorization (enum ame_variant) as a template parameter for the
+// GEMV-worker sweep of config 5 (MODE 2), so each variant's kernel carries only
+// its own code (as the v3 sweep, ame_sweep3.hip); -1 = read from dims.variant
+template <int R, int MODE, int VAR = -1>
 __global__ void __launch_bounds__(AME_NT)
 ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     // MODE 2: seven GEMV workers per slice (kind 22); MODE 3: four, pipelined (kind 23)
@@ -604,7 +607,8 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
     }
     const int tl = slice, tg = dm.t_begin + tl;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const bool is_naive = dm.variant == AME_NAIVE, is_bad = dm.variant == AME_BAD;
+    const bool is_naive = (VAR >= 0) ? (VAR == AME_NAIVE) : (dm.variant == AME_NAIVE);
+    const bool is_bad = (VAR >= 0) ? (VAR == AME_BAD) : (dm.variant == AME_BAD);
 
     const SweepLds L = sweep_lds_layout(n, R, MODE != 0 ? 1 : 0, WK ? 1 : 0);
     double* K = (double*)(smem + L.oK);          // D x KS
@@ -1940,7 +1944,13 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
 template <int R, int MODE>
 static int launch_sweep_t(const ame_dims* dm, const ame_sweep_args* a, hipStream_t st) {
     const long long lds = ame_v2_mode_lds(dm->n, R, MODE);
-    auto kern = ame_sweep_kernel<R, MODE>;
+    void (*kern)(ame_dims, ame_sweep_args);
+    if constexpr (MODE == 2)   // per-variant kernels (config 5's sweep)
+        kern = dm->variant == AME_NAIVE ? ame_sweep_kernel<R, MODE, AME_NAIVE>
+             : dm->variant == AME_BAD   ? ame_sweep_kernel<R, MODE, AME_BAD>
+                                        : ame_sweep_kernel<R, MODE, AME_GOOD>;
+    else
+        kern = ame_sweep_kernel<R, MODE>;
     if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
         hipSuccess)
         return -2;
@@ -1961,7 +1971,8 @@ template <int R, int MODE>
 static int sweep_occupancy_t(int n) {
     const long long lds = ame_v2_mode_lds(n, R, MODE);
     if (lds > AME_LDS_MAX) return 0;
-    auto kern = ame_sweep_kernel<R, MODE>;
+    // the variants of MODE 2 share the launch shape; the good one stands for them
+    auto kern = ame_sweep_kernel<R, MODE, MODE == 2 ? AME_GOOD : -1>;
     if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
         hipSuccess)
         return 0;

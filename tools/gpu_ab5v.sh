@@ -1,0 +1,12 @@
+#!/bin/bash
+# Same-box A/B of two r=32 builds at config 5's rank shape for the three variants.
+# usage: TAG ROUNDS LIB_A LIB_B
+set -o pipefail
+TAG=$1; ROUNDS=$2; A=$3; B=$4
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+OUT=gpurun_out/$TAG; mkdir -p $OUT
+for V in good naive bad; do
+  timeout -k 10 400 python -u tools/ab_v3.py $A $B --rounds $ROUNDS -- --n 4096 --t-per-gpu 32 --latent-dim 32 \
+     --steps 8 --warmup 2 --variant $V > $OUT/ab_$V.txt 2>&1 || { echo "ab $V failed"; tail -30 $OUT/ab_$V.txt; exit 1; }
+  echo "$V:"; grep median $OUT/ab_$V.txt
+done
