@@ -175,24 +175,26 @@ __device__ __forceinline__ void wave_lds_sync() {
 // rows per lane; KH = 2 only for D > 64); every lane gets all NV sums.  The
 // lane's rows are added, then one 64-lane reduce-scatter (permlane swaps +
 // DPP, fixed tree: deterministic) leaves sum v on one lane, which writes it
-// to LDS for the others.  NV <= 64.
-template <int NV, int D, int KH>
+// to LDS for the others.  Only the first NR <= NV sums are formed (the rest of
+// out is left alone).  NV <= 64.
+template <int NV, int D, int KH, int NR = NV>
 __device__ __forceinline__ void wave_multidot(const double (&pv)[KH][NV], double (&out)[NV],
                                               double* red /* unused */, double* sums, int lane) {
+    static_assert(NR <= NV, "wave_multidot: NR > NV");
     (void)red;
-    double v[NV];
+    double v[NR];
 #pragma unroll
-    for (int q = 0; q < NV; ++q) {
+    for (int q = 0; q < NR; ++q) {
         v[q] = pv[0][q];
 #pragma unroll
         for (int h = 1; h < KH; ++h) v[q] += pv[h][q];
     }
     int idx;
-    const double s = ame::wave_reduce_scatter<NV>(v, lane, idx);
-    if (idx < NV) sums[idx] = s;
+    const double s = ame::wave_reduce_scatter<NR>(v, lane, idx);
+    if (idx < NR) sums[idx] = s;
     wave_lds_sync();
 #pragma unroll
-    for (int qq = 0; qq < NV; ++qq) out[qq] = sums[qq];
+    for (int qq = 0; qq < NR; ++qq) out[qq] = sums[qq];
     wave_lds_sync();
 }
 
@@ -1605,7 +1607,10 @@ ame_sweep_kernel(ame_dims dm, ame_sweep_args a) {
                     pr[h][10] = jp0[h] * ua[h]; pr[h][11] = jp1[h] * ua[h];
                     pr[h][12] = jp0[h] * uM[h]; pr[h][13] = jp1[h] * uM[h];
                 }
-                wave_multidot<14, D, KH>(pr, o, red, scal, lane);
+                // sums 10-13 serve the bad variant only: a kernel instantiated for
+                // good / naive reduces 10 (13 pair steps of the tree instead of 16)
+                constexpr int NR = (VAR == AME_GOOD || VAR == AME_NAIVE) ? 10 : 14;
+                wave_multidot<14, D, KH, NR>(pr, o, red, scal, lane);
                 STAMPW(8, 0);
                 M22 Mm = {Rm.a + o[0], Rm.b + 0.5 * (o[1] + o[2]), 0.0, Rm.d + o[3]};
                 Mm.c = Mm.b;

@@ -725,26 +725,28 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
                 kj1 = s1a + s1b;
             }
             STAMP3(1);
-            // one reduction per step: a1(4) a2(4) c(4) e(2) jy(4) eA(2) ny(4), and the
-            // dots that do not involve mu_{i-1}: b1(2) b2(2) f1(4) f2(4) b1A(2) b2A(2)
+            // one reduction per step: a1(4) a2(4) c(4) e(2) jy(4) ny(4), and the
+            // dots that do not involve mu_{i-1}: b1(2) b2(2) f1(4) f2(4); the bad
+            // variant adds eA(2) b1A(2) b2A(2) at the end (34 values, 40 for bad:
+            // 37 pair steps of the tree instead of 41)
             // (W, X of the previous step, g_i and node i+1's J entries are this
             // lane's own registers; until round 3 a helper wave formed them, "HX",
             // and the solver waited for it: profiles/r03_v3_ab_hx_in_solver.txt)
-            constexpr int NV = 40;
+            constexpr int NV = is_bad ? 40 : 34;
             double pr[NV];
             pr[0] = Wp0 * J0; pr[1] = Wp0 * J1; pr[2] = Wp1 * J0; pr[3] = Wp1 * J1;       // a1[p][q]
             pr[4] = Xp0 * J0; pr[5] = Xp0 * J1; pr[6] = Xp1 * J0; pr[7] = Xp1 * J1;       // a2[p][q]
             pr[8] = J0 * kj0; pr[9] = J0 * kj1; pr[10] = J1 * kj0; pr[11] = J1 * kj1;     // c[q][p]
             pr[12] = J0 * v; pr[13] = J1 * v;                                             // e[q]
             pr[14] = J0 * yv0; pr[15] = J0 * yv1; pr[16] = J1 * yv0; pr[17] = J1 * yv1;   // jy[q][p]
-            pr[18] = J0 * vA; pr[19] = J1 * vA;                                           // eA[q]
-            pr[20] = nq0 * yv0; pr[21] = nq0 * yv1; pr[22] = nq1 * yv0; pr[23] = nq1 * yv1;   // ny[q][p]
-            {
+            pr[18] = nq0 * yv0; pr[19] = nq0 * yv1; pr[20] = nq1 * yv0; pr[21] = nq1 * yv1;   // ny[q][p]
+            pr[22] = Wp0 * g; pr[23] = Wp1 * g; pr[24] = Xp0 * g; pr[25] = Xp1 * g;           // b1, b2
+            pr[26] = Wp0 * nq0; pr[27] = Wp0 * nq1; pr[28] = Wp1 * nq0; pr[29] = Wp1 * nq1;   // f1[p][q]
+            pr[30] = Xp0 * nq0; pr[31] = Xp0 * nq1; pr[32] = Xp1 * nq0; pr[33] = Xp1 * nq1;   // f2[p][q]
+            if constexpr (is_bad) {
                 const double gA = (k < 2) ? g : 0.0;
-                pr[24] = Wp0 * g; pr[25] = Wp1 * g; pr[26] = Xp0 * g; pr[27] = Xp1 * g;           // b1, b2
-                pr[28] = Wp0 * nq0; pr[29] = Wp0 * nq1; pr[30] = Wp1 * nq0; pr[31] = Wp1 * nq1;   // f1[p][q]
-                pr[32] = Xp0 * nq0; pr[33] = Xp0 * nq1; pr[34] = Xp1 * nq0; pr[35] = Xp1 * nq1;   // f2[p][q]
-                pr[36] = Wp0 * gA; pr[37] = Wp1 * gA; pr[38] = Xp0 * gA; pr[39] = Xp1 * gA;       // b1A, b2A
+                pr[34] = J0 * vA; pr[35] = J1 * vA;                                           // eA[q]
+                pr[36] = Wp0 * gA; pr[37] = Wp1 * gA; pr[38] = Xp0 * gA; pr[39] = Xp1 * gA;   // b1A, b2A
             }
             {
                 int idx;
@@ -760,14 +762,12 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             const Mat2 cc = m2(o[8], o[9], o[10], o[11]);
             const V2 e = {o[12], o[13]};
             const Mat2 jy = m2(o[14], o[15], o[16], o[17]);
-            const V2 eA = {o[18], o[19]};
-            const Mat2 ny = m2(o[20], o[21], o[22], o[23]);
+            const Mat2 ny = m2(o[18], o[19], o[20], o[21]);
             STAMP3(2);
             STAMP3(3);
-            const V2 b1 = {o[24], o[25]}, b2 = {o[26], o[27]};
-            const Mat2 f1 = m2(o[28], o[29], o[30], o[31]);
-            const Mat2 f2 = m2(o[32], o[33], o[34], o[35]);
-            const V2 b1A = {o[36], o[37]}, b2A = {o[38], o[39]};
+            const V2 b1 = {o[22], o[23]}, b2 = {o[24], o[25]};
+            const Mat2 f1 = m2(o[26], o[27], o[28], o[29]);
+            const Mat2 f2 = m2(o[30], o[31], o[32], o[33]);
             // raw y_{i,i-1}
             double y0 = 0, y1 = 0;
             if (has_prev) { y0 = (double)yst[(i & 3) * 4 + 0]; y1 = (double)yst[(i & 3) * 4 + 1]; }
@@ -790,9 +790,11 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             const double kn0 = yv0 - (Lp0 * f1.a + Lp1 * f1.c) + (Gp0 * f2.a + Gp1 * f2.c);
             const double kn1 = yv1 - (Lp0 * f1.b + Lp1 * f1.d) + (Gp0 * f2.b + Gp1 * f2.d);
             double mus;
-            if (!is_bad) {
+            if constexpr (!is_bad) {
                 mus = u + W0 * cvec.x + W1 * cvec.y;
             } else {
+                const V2 eA = {o[34], o[35]};
+                const V2 b1A = {o[36], o[37]}, b2A = {o[38], o[39]};
                 const double uA = vA - (Lp0 * b1A.x + Lp1 * b1A.y) + (Gp0 * b2A.x + Gp1 * b2A.y);
                 const V2 s1 = mtv(a1, mv(Mip, b1A)), s2 = mtv(a2, mv(Sip, b2A));
                 const V2 JuA = {eA.x - s1.x + s2.x, eA.y - s1.y + s2.y};
