@@ -727,22 +727,38 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             STAMP3(1);
             // one reduction per step: a1(4) a2(4) c(4) e(2) jy(4) ny(4), and the
             // dots that do not involve mu_{i-1}: b1(2) b2(2) f1(4) f2(4); the bad
-            // variant adds eA(2) b1A(2) b2A(2) at the end (34 values, 40 for bad:
-            // 37 pair steps of the tree instead of 41)
+            // variant adds eA(2) b1A(2) b2A(2) at the end (40 values, 41 pair steps
+            // of the tree; good 34, 37 pair steps).  c = J B J^T and ny = Jn B Jn^T
+            // are symmetric and only bad reads them other than through sym(): the
+            // naive instance reduces their upper triangles (the off-diagonal as the
+            // lanes' mean of both products), 32 values, 32 pair steps.  The same
+            // packing measured 0.8 % slower for good, 5.7 % faster for naive
+            // (profiles/r06_ab_sym_pack.txt), so only naive packs
             // (W, X of the previous step, g_i and node i+1's J entries are this
             // lane's own registers; until round 3 a helper wave formed them, "HX",
             // and the solver waited for it: profiles/r03_v3_ab_hx_in_solver.txt)
-            constexpr int NV = is_bad ? 40 : 34;
+            constexpr bool pack = is_naive;
+            constexpr int NV = is_bad ? 40 : (pack ? 32 : 34);
+            constexpr int IE = pack ? 11 : 12, IJY = IE + 2, INY = IJY + 4;
+            constexpr int IB = INY + (pack ? 3 : 4), IF1 = IB + 4, IF2 = IF1 + 4;
             double pr[NV];
             pr[0] = Wp0 * J0; pr[1] = Wp0 * J1; pr[2] = Wp1 * J0; pr[3] = Wp1 * J1;       // a1[p][q]
             pr[4] = Xp0 * J0; pr[5] = Xp0 * J1; pr[6] = Xp1 * J0; pr[7] = Xp1 * J1;       // a2[p][q]
-            pr[8] = J0 * kj0; pr[9] = J0 * kj1; pr[10] = J1 * kj0; pr[11] = J1 * kj1;     // c[q][p]
-            pr[12] = J0 * v; pr[13] = J1 * v;                                             // e[q]
-            pr[14] = J0 * yv0; pr[15] = J0 * yv1; pr[16] = J1 * yv0; pr[17] = J1 * yv1;   // jy[q][p]
-            pr[18] = nq0 * yv0; pr[19] = nq0 * yv1; pr[20] = nq1 * yv0; pr[21] = nq1 * yv1;   // ny[q][p]
-            pr[22] = Wp0 * g; pr[23] = Wp1 * g; pr[24] = Xp0 * g; pr[25] = Xp1 * g;           // b1, b2
-            pr[26] = Wp0 * nq0; pr[27] = Wp0 * nq1; pr[28] = Wp1 * nq0; pr[29] = Wp1 * nq1;   // f1[p][q]
-            pr[30] = Xp0 * nq0; pr[31] = Xp0 * nq1; pr[32] = Xp1 * nq0; pr[33] = Xp1 * nq1;   // f2[p][q]
+            if constexpr (!pack) {
+                pr[8] = J0 * kj0; pr[9] = J0 * kj1; pr[10] = J1 * kj0; pr[11] = J1 * kj1;     // c[q][p]
+            } else {
+                pr[8] = J0 * kj0; pr[9] = 0.5 * (J0 * kj1 + J1 * kj0); pr[10] = J1 * kj1;     // c, sym
+            }
+            pr[IE] = J0 * v; pr[IE + 1] = J1 * v;                                                 // e[q]
+            pr[IJY] = J0 * yv0; pr[IJY + 1] = J0 * yv1; pr[IJY + 2] = J1 * yv0; pr[IJY + 3] = J1 * yv1;   // jy[q][p]
+            if constexpr (!pack) {
+                pr[INY] = nq0 * yv0; pr[INY + 1] = nq0 * yv1; pr[INY + 2] = nq1 * yv0; pr[INY + 3] = nq1 * yv1;   // ny[q][p]
+            } else {
+                pr[INY] = nq0 * yv0; pr[INY + 1] = 0.5 * (nq0 * yv1 + nq1 * yv0); pr[INY + 2] = nq1 * yv1;   // ny, sym
+            }
+            pr[IB] = Wp0 * g; pr[IB + 1] = Wp1 * g; pr[IB + 2] = Xp0 * g; pr[IB + 3] = Xp1 * g;           // b1, b2
+            pr[IF1] = Wp0 * nq0; pr[IF1 + 1] = Wp0 * nq1; pr[IF1 + 2] = Wp1 * nq0; pr[IF1 + 3] = Wp1 * nq1;   // f1[p][q]
+            pr[IF2] = Xp0 * nq0; pr[IF2 + 1] = Xp0 * nq1; pr[IF2 + 2] = Xp1 * nq0; pr[IF2 + 3] = Xp1 * nq1;   // f2[p][q]
             if constexpr (is_bad) {
                 const double gA = (k < 2) ? g : 0.0;
                 pr[34] = J0 * vA; pr[35] = J1 * vA;                                           // eA[q]
@@ -759,15 +775,16 @@ ame_sweep3_kernel(ame_dims dm, ame_sweep_args a) {
             for (int q = 0; q < NV; ++q) o[q] = red[q];
             const Mat2 a1 = m2(o[0], o[1], o[2], o[3]);
             const Mat2 a2 = m2(o[4], o[5], o[6], o[7]);
-            const Mat2 cc = m2(o[8], o[9], o[10], o[11]);
-            const V2 e = {o[12], o[13]};
-            const Mat2 jy = m2(o[14], o[15], o[16], o[17]);
-            const Mat2 ny = m2(o[18], o[19], o[20], o[21]);
+            const Mat2 cc = !pack ? m2(o[8], o[9], o[10], o[11]) : m2(o[8], o[9], o[9], o[10]);
+            const V2 e = {o[IE], o[IE + 1]};
+            const Mat2 jy = m2(o[IJY], o[IJY + 1], o[IJY + 2], o[IJY + 3]);
+            const Mat2 ny = !pack ? m2(o[INY], o[INY + 1], o[INY + 2], o[INY + 3])
+                                   : m2(o[INY], o[INY + 1], o[INY + 1], o[INY + 2]);
             STAMP3(2);
             STAMP3(3);
-            const V2 b1 = {o[22], o[23]}, b2 = {o[24], o[25]};
-            const Mat2 f1 = m2(o[26], o[27], o[28], o[29]);
-            const Mat2 f2 = m2(o[30], o[31], o[32], o[33]);
+            const V2 b1 = {o[IB], o[IB + 1]}, b2 = {o[IB + 2], o[IB + 3]};
+            const Mat2 f1 = m2(o[IF1], o[IF1 + 1], o[IF1 + 2], o[IF1 + 3]);
+            const Mat2 f2 = m2(o[IF2], o[IF2 + 1], o[IF2 + 2], o[IF2 + 3]);
             // raw y_{i,i-1}
             double y0 = 0, y1 = 0;
             if (has_prev) { y0 = (double)yst[(i & 3) * 4 + 0]; y1 = (double)yst[(i & 3) * 4 + 1]; }
